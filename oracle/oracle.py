@@ -1,0 +1,153 @@
+"""ctypes wrapper of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+The oracle (sift_oracle.c) is an fp64 C restatement of the reference's
+algorithm, pinned against golden vectors produced by the reference itself
+(tests/golden).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may use it, as the checker / CPU baseline -- the product
+path (libsift_hip.so) never links or calls it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+CONV_2D = 0
+CONV_SEPARABLE = 1
+
+
+class OracleParams(ctypes.Structure):
+    _fields_ = [("num_octaves", ctypes.c_int), ("scales_per_octave", ctypes.c_int),
+                ("min_blur", ctypes.c_double), ("assumed_blur", ctypes.c_double),
+                ("min_interpixel_distance", ctypes.c_double)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        lp = ctypes.POINTER(ctypes.c_long)
+        pp = ctypes.POINTER(OracleParams)
+        L.oracle_octave_dims.restype = ctypes.c_long
+        L.oracle_octave_dims.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ip]
+        L.oracle_schedule.argtypes = [pp, dp, dp]
+        L.oracle_scale_space.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int,
+                                         pp, ctypes.c_int, dp]
+        L.oracle_dog.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, dp]
+        L.oracle_find_extrema.restype = ctypes.c_long
+        L.oracle_find_extrema.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, ip, dp, ctypes.c_long, lp]
+        L.oracle_refine.restype = ctypes.c_long
+        L.oracle_refine.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, ip, dp, ctypes.c_long, dp,
+                                    ctypes.c_long, lp]
+        L.oracle_detect_count.restype = ctypes.c_long
+        L.oracle_detect_count.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int,
+                                          pp, ctypes.c_int, lp]
+        _lib = L
+    return _lib
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def make_params(num_octaves, scales_per_octave, min_blur=0.8, assumed_blur=0.5,
+                min_interpixel_distance=0.5):
+    return OracleParams(int(num_octaves), int(scales_per_octave), float(min_blur),
+                        float(assumed_blur), float(min_interpixel_distance))
+
+
+def octave_dims(W, H, O):
+    d = np.zeros(2 * O, dtype=np.int32)
+    lib().oracle_octave_dims(W, H, O, _ptr(d, ctypes.c_int32))
+    return [(int(d[2 * o]), int(d[2 * o + 1])) for o in range(O)]
+
+
+def schedule(p):
+    NS = p.scales_per_octave + 3
+    blur = np.zeros(p.num_octaves * NS)
+    sig = np.zeros(p.num_octaves * NS)
+    lib().oracle_schedule(ctypes.byref(p), _ptr(blur, ctypes.c_double), _ptr(sig, ctypes.c_double))
+    return blur.reshape(-1, NS), sig.reshape(-1, NS)
+
+
+def split_pyramid(flat, dims, per_octave):
+    out, off = [], 0
+    for (h, w) in dims:
+        n = h * w * per_octave
+        out.append(flat[off:off + n].reshape(per_octave, h, w))
+        off += n
+    return out
+
+
+class OracleRun:
+    """Full oracle pipeline on one image; keeps flat fp64 pyramids."""
+
+    def __init__(self, img, p, mode=CONV_SEPARABLE):
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        H, W = img.shape
+        self.W, self.H, self.p = W, H, p
+        O, S = p.num_octaves, p.scales_per_octave
+        self.dims = octave_dims(W, H, O)
+        P = sum(h * w for h, w in self.dims)
+        L = lib()
+        self.gauss_flat = np.zeros(P * (S + 3))
+        L.oracle_scale_space(_ptr(img, ctypes.c_float), W, H, ctypes.byref(p), mode,
+                             _ptr(self.gauss_flat, ctypes.c_double))
+        self.dog_flat = np.zeros(P * (S + 2))
+        L.oracle_dog(ctypes.byref(p), W, H, _ptr(self.gauss_flat, ctypes.c_double),
+                     _ptr(self.dog_flat, ctypes.c_double))
+        self.gauss = split_pyramid(self.gauss_flat, self.dims, S + 3)
+        self.dog = split_pyramid(self.dog_flat, self.dims, S + 2)
+        low = ctypes.c_long(0)
+        n = L.oracle_find_extrema(ctypes.byref(p), W, H, _ptr(self.dog_flat, ctypes.c_double),
+                                  None, None, 0, ctypes.byref(low))
+        self.cand_rec = np.zeros((max(n, 1), 4), dtype=np.int32)
+        self.cand_val = np.zeros(max(n, 1))
+        L.oracle_find_extrema(ctypes.byref(p), W, H, _ptr(self.dog_flat, ctypes.c_double),
+                              _ptr(self.cand_rec, ctypes.c_int32), _ptr(self.cand_val, ctypes.c_double),
+                              n, ctypes.byref(low))
+        self.cand_rec, self.cand_val = self.cand_rec[:n], self.cand_val[:n]
+        self.n_low = int(low.value)
+        self.refined, self.n_singular = self.refine(self.cand_rec, self.cand_val)
+
+    def refine(self, rec, val):
+        rec = np.ascontiguousarray(rec, dtype=np.int32)
+        val = np.ascontiguousarray(val, dtype=np.float64)
+        n = rec.shape[0]
+        out = np.zeros((max(n, 1), 8))
+        sing = ctypes.c_long(0)
+        k = lib().oracle_refine(ctypes.byref(self.p), self.W, self.H,
+                                _ptr(self.dog_flat, ctypes.c_double), _ptr(rec, ctypes.c_int32),
+                                _ptr(val, ctypes.c_double), n, _ptr(out, ctypes.c_double), n,
+                                ctypes.byref(sing))
+        return out[:k], int(sing.value)
+
+    def candidates(self):
+        """(N,5) [octave, scale, x, y, value] in reference order."""
+        c = np.zeros((self.cand_rec.shape[0], 5))
+        c[:, :4] = self.cand_rec
+        c[:, 4] = self.cand_val
+        return c
+
+
+def detect_count(img, p, mode=CONV_2D):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = img.shape
+    nc = ctypes.c_long(0)
+    nk = lib().oracle_detect_count(_ptr(img, ctypes.c_float), W, H, ctypes.byref(p), mode,
+                                   ctypes.byref(nc))
+    return int(nk), int(nc.value)
