@@ -1,0 +1,197 @@
+/*
+ * sift_hip.h -- C ABI of the MI355X (gfx950) SIFT scale-space extrema path.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (bingjetli/sift-scale-space-extrema-detection).  The reference exposes the
+ * path as a Web-Worker message protocol (src/worker.js:5-98 helpers,
+ * background.js:14-50 dispatcher); every entry point below names the
+ * reference function whose behaviour it reproduces.  Plain C types only: no
+ * C++ or torch types cross this boundary.  The Node N-API addon
+ * (sift-scale-space-extrema-detection_amd/napi/sift_napi.c) and the Python
+ * ctypes binding bind exactly these symbols.
+ *
+ * Threading: one sift_ctx per host thread; a ctx is not re-entrant; distinct
+ * ctxs are independent.  Every call is synchronous with respect to the ctx's
+ * HIP stream unless its name ends in _async.
+ *
+ * Numerics: Gaussian weights and every convolution accumulate in fp64 (the
+ * reference computes in JS Number = fp64); Gaussian and DoG planes are
+ * handed out as fp32 (the ImageData-shaped Float32 contract); octave seeds
+ * stay fp64 on device; extrema decisions and refinement are fp64 and exact
+ * with respect to the fp64 pyramid (fp32 ties are re-decided in fp64).
+ */
+#ifndef SIFT_HIP_H
+#define SIFT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIFT_ABI_VERSION 1
+
+/* Status codes.  Every function returns one of these. */
+enum {
+  SIFT_OK = 0,
+  SIFT_E_ARG = -1,        /* invalid argument (null pointer, bad size, bad index)   */
+  SIFT_E_HIP = -2,        /* HIP runtime error; see sift_last_error()               */
+  SIFT_E_CAPACITY = -3,   /* output buffer too small; *n_out holds the needed count */
+  SIFT_E_STATE = -4,      /* stage called before the stage it depends on            */
+  SIFT_E_SINGULAR = -5,   /* refinement met a Hessian with |det| < DBL_EPSILON: the
+                             reference throws a TypeError there (matrix2d.js:482 ->
+                             :455); outputs for every other candidate are still
+                             written and *n_singular counts the offenders           */
+  SIFT_E_UNSUPPORTED = -6 /* configuration outside this build's limits              */
+};
+
+/* Plane kinds for sift_get_plane / sift_get_blur_level. */
+enum { SIFT_PLANE_GAUSS = 0, SIFT_PLANE_DOG = 1 };
+
+/* sift_params.flags */
+enum {
+  SIFT_F_SKIP_GAUSS_PLANES = 1 << 0, /* do not materialise Gaussian planes (seeds still kept) */
+  SIFT_F_SKIP_DOG_PLANES = 1 << 1    /* reserved: DoG planes are needed by refinement today   */
+};
+
+/* Parameters of the pipeline.  Names and defaults follow
+ * src/worker.js:29-98 (workerComputeGaussianScaleSpace / ...Refine...). */
+typedef struct {
+  int num_octaves;                /* number_of_octaves        default 5   (worker.js:33) */
+  int scales_per_octave;          /* scales_per_octave        default 3   (worker.js:34) */
+  double min_blur;                /* min_blur_level           default 0.8 (worker.js:35) */
+  double assumed_blur;            /* assumed_blur             default 0.5 (worker.js:36) */
+  double min_interpixel_distance; /* min_interpixel_distance  default 0.5 (worker.js:88) */
+  int flags;                      /* SIFT_F_*                 default 0                  */
+} sift_params;
+
+/* One candidate extremum, reference order (octave, scale, y, x):
+ * background.js:433-436 {scaleLevel, localExtremas:[{x, y, value}]}. */
+typedef struct {
+  int32_t octave;
+  int32_t scale; /* scaleLevel: DoG index 1..S */
+  int32_t x;
+  int32_t y;
+  double value; /* DoG value at (x, y) */
+} sift_extremum;
+
+/* One refined keypoint: background.js:619-628. */
+typedef struct {
+  int32_t octave;
+  int32_t scale_level;
+  int32_t local_x;
+  int32_t local_y;
+  double abs_x;
+  double abs_y;
+  double abs_sigma;
+  double interp_value;
+} sift_keypoint;
+
+/* Per-stage device timings of the last call chain, milliseconds. */
+typedef struct {
+  double gauss_dog_ms; /* Gaussian + DoG kernels (all octaves)              */
+  double extrema_ms;   /* extrema scan + ordering + exact tie resolution    */
+  double refine_ms;    /* refinement + compaction                           */
+  double h2d_ms;       /* input upload (0 for the device-pointer entry)     */
+} sift_timings;
+
+int sift_abi_version(void);
+int sift_params_default(sift_params *p);
+
+/* Context: owns one HIP stream and device-resident pyramids on `device`. */
+int sift_ctx_create(int device, struct sift_ctx **out);
+int sift_ctx_destroy(struct sift_ctx *ctx);
+const char *sift_last_error(struct sift_ctx *ctx);
+
+/* Offset sigma and blur level of every (octave, scale) for these params,
+ * background.js:89-177.  Arrays are num_octaves*(scales_per_octave+3);
+ * sigma 0 marks the un-blurred octave seed.  Pure host math. */
+int sift_schedule(const sift_params *p, double *blur_levels, double *offset_sigmas);
+
+/* Octave plane dims for a W x H input: dims[2o] = rows, dims[2o+1] = cols.
+ * Pure host math (matrix2d.js:112-138 resize rules). */
+int sift_octave_dims(int width, int height, int num_octaves, int *dims);
+
+/* computeGaussianScaleSpace (background.js:71-237) fused with
+ * computeDifferenceOfGaussians (background.js:258-354).  `img` is a gray
+ * row-major Float32 host image (ImageData-shaped, stride in pixels).
+ * `offset_sigmas` may be NULL (schedule computed here) or supply the
+ * num_octaves*(S+3) offset sigmas computed by the caller (e.g. in JS with
+ * Math.pow, so the schedule is bit-identical to the reference's). */
+int sift_build_scale_space(struct sift_ctx *ctx, const float *img, int width, int height,
+                           size_t stride_px, const sift_params *p, const double *offset_sigmas);
+
+/* Same, with `d_img` already resident in device memory of ctx's device. */
+int sift_build_scale_space_device(struct sift_ctx *ctx, const float *d_img, int width,
+                                  int height, size_t stride_px, const sift_params *p,
+                                  const double *offset_sigmas);
+
+int sift_get_dims(struct sift_ctx *ctx, int octave, int *rows, int *cols);
+int sift_get_blur_level(struct sift_ctx *ctx, int kind, int octave, int scale, double *blur);
+
+/* Copy one plane to host memory owned by the caller (cap in pixels). */
+int sift_get_plane(struct sift_ctx *ctx, int kind, int octave, int scale, float *dst,
+                   size_t cap_px);
+
+/* Replace the context's DoG pyramid with caller-supplied planes (for callers
+ * that hand findCandidateKeypoints / refineCandidateKeypoints a pyramid this
+ * context did not build).  `planes` is octave-major, (S+2) planes per
+ * octave, each rows*cols fp32 in the dims sift_octave_dims gives. */
+int sift_load_dog(struct sift_ctx *ctx, const float *planes, int width, int height,
+                  const sift_params *p);
+
+/* Replace the Gaussian pyramid with caller planes ((S+3) per octave) and
+ * recompute the DoG from them: computeDifferenceOfGaussians on a foreign
+ * scale space (background.js:258-354, sift.js:154-188). */
+int sift_load_scale_space(struct sift_ctx *ctx, const float *planes, int width, int height,
+                          const sift_params *p);
+
+/* findCandidateKeypoints (background.js:359-450 + sift.js:212-316).
+ * Strict 26-neighbour extrema of DoG scales 1..S with |v| >= 0.8*thr, in
+ * reference order.  *n_low_contrast counts extrema failing 0.8*thr.
+ * SIFT_E_CAPACITY: *n_out = required count, nothing written. */
+int sift_find_extrema(struct sift_ctx *ctx, sift_extremum *out, size_t cap, size_t *n_out,
+                      size_t *n_low_contrast);
+
+/* refineCandidateKeypoints (background.js:455-685) on the candidates of the
+ * last sift_find_extrema (or sift_set_candidates).  Output keeps reference
+ * order and duplicates. */
+int sift_refine(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out,
+                size_t *n_singular);
+
+/* Copy the candidates / keypoints of the last find / refine / detect without
+ * recomputing (cap in records; SIFT_E_CAPACITY if too small). */
+int sift_copy_candidates(struct sift_ctx *ctx, sift_extremum *out, size_t cap, size_t *n_out);
+int sift_copy_keypoints(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out);
+
+/* Use caller-supplied candidates (reference order) for the next sift_refine. */
+int sift_set_candidates(struct sift_ctx *ctx, const sift_extremum *cand, size_t n);
+
+/* Whole path in one call: build + extrema + refine.  Keypoints stay on
+ * device when out == NULL (counts still returned). */
+int sift_detect(struct sift_ctx *ctx, const float *img, int width, int height, size_t stride_px,
+                const sift_params *p, sift_keypoint *out, size_t cap, size_t *n_out);
+int sift_detect_device(struct sift_ctx *ctx, const float *d_img, int width, int height,
+                       size_t stride_px, const sift_params *p, sift_keypoint *out, size_t cap,
+                       size_t *n_out);
+
+/* Counts of the last detect / find / refine: candidates, low-contrast
+ * extrema, refined keypoints, singular Hessians, exact fp64 re-decisions. */
+int sift_last_counts(struct sift_ctx *ctx, size_t *n_candidates, size_t *n_low_contrast,
+                     size_t *n_keypoints, size_t *n_singular, size_t *n_exact);
+
+int sift_last_timings(struct sift_ctx *ctx, sift_timings *t);
+
+/* Raw device pointers (for in-process consumers that stay on device, e.g.
+ * the RCCL all-gather of keypoints).  Valid until the next build/detect. */
+int sift_device_keypoints(struct sift_ctx *ctx, const sift_keypoint **d_kp, size_t *n);
+void *sift_stream(struct sift_ctx *ctx);
+
+/* Wait for all work queued on ctx's stream. */
+int sift_synchronize(struct sift_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIFT_HIP_H */

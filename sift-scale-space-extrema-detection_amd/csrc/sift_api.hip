@@ -1,0 +1,780 @@
+// C ABI of libsift_hip.so (include/sift_hip.h): context, schedule, stage
+// orchestration on one HIP stream.  The stage functions mirror the
+// reference's worker stages (background.js:71 / :258 / :359 / :455).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/sift_hip.h"
+#include "sift_kernels.h"
+
+using namespace sift;
+
+namespace {
+
+// Grow-only device buffer.
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t need) {
+    if (need <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t want = need + need / 4 + 256;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+double js_round(double x) {
+  double f = std::floor(x);
+  return (x - f >= 0.5) ? f + 1.0 : f;
+}
+
+enum DogSource { kNone = 0, kNative = 1, kForeign = 2 };
+
+}  // namespace
+
+struct sift_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  sift_params p{};
+  int W = 0, H = 0;
+  std::vector<int> dims;           // 2*O
+  std::vector<double> blur, sigma; // O*NS
+  Pyramid P{};
+  int dog_source = kNone;
+  bool have_gauss = false;
+  bool have_cand = false;
+  size_t n_cand = 0, n_low = 0, n_kp = 0, n_sing = 0, n_exact = 0;
+  // device memory
+  DBuf img, seeds, gauss, dog, wts;
+  DBuf ext_keys, ext_pay, srt_keys, srt_pay;   // extrema records
+  DBuf keep, pos, value, flagged;              // candidate ordering
+  DBuf cand_key, cand_val;                     // ordered candidates
+  DBuf status, kp_tmp, kp, uncertain;          // refinement
+  DBuf counters, temp;
+  unsigned* h_counters = nullptr;              // pinned mirror of counters
+  hipEvent_t ev[8]{};
+  sift_timings tm{};
+};
+
+#define HIPCHK(call)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess) {                                                                 \
+      ctx->err = std::string(#call) + ": " + hipGetErrorString(e_);                         \
+      return SIFT_E_HIP;                                                                    \
+    }                                                                                       \
+  } while (0)
+
+static int set_err(sift_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+static int check_params(const sift_params* p) {
+  if (!p) return SIFT_E_ARG;
+  if (p->num_octaves < 1 || p->num_octaves > kMaxOctaves) return SIFT_E_UNSUPPORTED;
+  if (p->scales_per_octave < 1 || p->scales_per_octave + 3 > kMaxScales) return SIFT_E_UNSUPPORTED;
+  if (!(p->min_blur > 0) || !(p->assumed_blur >= 0) || !(p->min_interpixel_distance > 0)) return SIFT_E_ARG;
+  return SIFT_OK;
+}
+
+extern "C" {
+
+int sift_abi_version(void) { return SIFT_ABI_VERSION; }
+
+int sift_params_default(sift_params* p) {
+  if (!p) return SIFT_E_ARG;
+  p->num_octaves = 5;         // worker.js:33
+  p->scales_per_octave = 3;   // worker.js:34
+  p->min_blur = 0.8;          // worker.js:35
+  p->assumed_blur = 0.5;      // worker.js:36
+  p->min_interpixel_distance = 0.5;  // worker.js:88
+  p->flags = 0;
+  return SIFT_OK;
+}
+
+int sift_octave_dims(int width, int height, int num_octaves, int* dims) {
+  if (width < 1 || height < 1 || num_octaves < 1 || !dims) return SIFT_E_ARG;
+  int h = 2 * height, w = 2 * width;  // background.js:84 (2x upsample)
+  for (int o = 0; o < num_octaves; ++o) {
+    if (o > 0) { h = (h + 1) / 2; w = (w + 1) / 2; }  // background.js:118
+    dims[2 * o] = h;
+    dims[2 * o + 1] = w;
+  }
+  return SIFT_OK;
+}
+
+int sift_schedule(const sift_params* p, double* blur, double* sigma) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  if (!blur || !sigma) return SIFT_E_ARG;
+  // background.js:89-177
+  const int S = p->scales_per_octave, NS = S + 3;
+  const double k = std::pow(2.0, 1.0 / S);
+  double base_blur = p->min_blur;
+  for (int o = 0; o < p->num_octaves; ++o) {
+    for (int s = 0; s < NS; ++s) {
+      if (o > 0 && s == 0) {
+        base_blur = blur[(o - 1) * NS + S];
+        blur[o * NS] = base_blur;
+        sigma[o * NS] = 0.0;
+      } else {
+        const double target = base_blur * std::pow(k, (double)s);
+        const double from = o == 0 ? p->assumed_blur : base_blur;
+        blur[o * NS + s] = target;
+        sigma[o * NS + s] = std::sqrt((target * target) - (from * from));
+      }
+    }
+  }
+  return SIFT_OK;
+}
+
+int sift_ctx_create(int device, sift_ctx** out) {
+  if (!out) return SIFT_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return SIFT_E_HIP;
+  if (device < 0 || device >= n) return SIFT_E_ARG;
+  sift_ctx* ctx = new sift_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->h_counters, 64 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
+      ctx->counters.ensure(64 * sizeof(unsigned)) != hipSuccess) {
+    delete ctx;
+    return SIFT_E_HIP;
+  }
+  for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  *out = ctx;
+  return SIFT_OK;
+}
+
+int sift_ctx_destroy(sift_ctx* ctx) {
+  if (!ctx) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->ext_keys,
+                  &ctx->ext_pay, &ctx->srt_keys, &ctx->srt_pay, &ctx->keep, &ctx->pos,
+                  &ctx->value, &ctx->flagged, &ctx->cand_key, &ctx->cand_val, &ctx->status,
+                  &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->counters, &ctx->temp};
+  for (DBuf* b : bufs) b->release();
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return SIFT_OK;
+}
+
+const char* sift_last_error(sift_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void* sift_stream(sift_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int sift_synchronize(sift_ctx* ctx) {
+  if (!ctx) return SIFT_E_ARG;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Geometry, schedule and weights (host), background.js:71-177 + sift.js:31-67.
+// ---------------------------------------------------------------------------
+static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, const double* sig_in,
+                          bool need_weights) {
+  int rc = check_params(p);
+  if (rc) return set_err(ctx, rc, "invalid or unsupported parameters");
+  if (W < 1 || H < 1) return set_err(ctx, SIFT_E_ARG, "empty image");
+  const int O = p->num_octaves, S = p->scales_per_octave, NS = S + 3, ND = S + 2;
+  ctx->p = *p;
+  ctx->W = W;
+  ctx->H = H;
+  ctx->dims.assign(2 * O, 0);
+  sift_octave_dims(W, H, O, ctx->dims.data());
+  ctx->blur.assign(O * NS, 0.0);
+  ctx->sigma.assign(O * NS, 0.0);
+  sift_schedule(p, ctx->blur.data(), ctx->sigma.data());
+  if (sig_in) {
+    for (int i = 0; i < O * NS; ++i) ctx->sigma[i] = sig_in[i];
+  }
+  Pyramid& P = ctx->P;
+  std::memset(&P, 0, sizeof(P));
+  P.O = O; P.S = S; P.NS = NS; P.ND = ND;
+  P.W = W; P.H = H;
+  const double thr = ((std::pow(2.0, 1.0 / S) - 1) / (std::pow(2.0, 1.0 / 3) - 1)) * 0.015;
+  P.thr = thr;             // background.js:572
+  P.pix_thr = thr * 0.8;   // sift.js:285-294
+  std::vector<double> w;
+  long long goff = 0, doff = 0, soff = 0;
+  unsigned long long koff = 0;
+  for (int o = 0; o < O; ++o) {
+    Octave& oc = P.oct[o];
+    oc.h = ctx->dims[2 * o];
+    oc.w = ctx->dims[2 * o + 1];
+    const long long plane = (long long)oc.h * oc.w;
+    oc.gauss_off = goff;
+    oc.dog_off = doff;
+    oc.seed_off = o > 0 ? soff : 0;
+    if (o > 0) soff += plane;
+    if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");
+    oc.key_off = (unsigned)koff;
+    koff += (unsigned long long)S * plane;
+    goff += NS * plane;
+    doff += ND * plane;
+    oc.rmax = 0;
+    for (int s = 0; s < NS; ++s) {
+      const double sg = ctx->sigma[o * NS + s];
+      int r = 0;
+      for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
+      oc.wofs[s] = (int)w.size();
+      if (o > 0 && s == 0) {
+        w.push_back(1.0);  // the un-blurred seed: exact copy
+      } else {
+        // sift.js:38-44: r = Math.round(3 sigma); the 2D kernel
+        // exp(((i^2+j^2)/s^2)*-0.5)/(2 pi s^2) / sum factors as w(i) w(j)
+        // with w(i) = exp((i^2/s^2)*-0.5) / sum_i exp(...).
+        r = (int)js_round(3.0 * sg);
+        std::vector<double> g(2 * r + 1);
+        double sum = 0.0;
+        for (int i = 0; i <= 2 * r; ++i) {
+          const double a = i - r;
+          g[i] = std::exp(((a * a) / (sg * sg)) * -0.5);
+          sum += g[i];
+        }
+        for (int i = 0; i <= 2 * r; ++i) w.push_back(g[i] / sum);
+      }
+      for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
+      oc.rad[s] = r;
+      oc.rmax = std::max(oc.rmax, r);
+    }
+  }
+  if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");
+  // LDS feasibility of the Gaussian kernel (strip of min(h, 32+2R) fp64 rows).
+  for (int o = 0; o < O; ++o)
+    if (gauss_lds_bytes(P.oct[o], false) > 160 * 1024)
+      return set_err(ctx, SIFT_E_UNSUPPORTED, "blur radius too large for one LDS strip");
+  if (need_weights) {
+    if (ctx->wts.ensure(w.size() * sizeof(double)) != hipSuccess)
+      return set_err(ctx, SIFT_E_HIP, "hipMalloc weights");
+    if (hipMemcpyAsync(ctx->wts.p, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice,
+                       ctx->stream) != hipSuccess)
+      return set_err(ctx, SIFT_E_HIP, "upload weights");
+    P.wts = ctx->wts.as<double>();
+  }
+  (void)soff;
+  return SIFT_OK;
+}
+
+static long long total_plane_px(const sift_ctx* ctx) {
+  long long t = 0;
+  for (int o = 0; o < ctx->P.O; ++o) t += (long long)ctx->P.oct[o].h * ctx->P.oct[o].w;
+  return t;
+}
+
+static int build_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
+                        size_t stride, const sift_params* p, const double* sig) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!img_host && !img_dev) return set_err(ctx, SIFT_E_ARG, "null image");
+  if (stride < (size_t)W) return set_err(ctx, SIFT_E_ARG, "stride < width");
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = setup_geometry(ctx, W, H, p, sig, true);
+  if (rc) return rc;
+  Pyramid& P = ctx->P;
+  const long long tot = total_plane_px(ctx);
+  const bool keep_gauss = !(p->flags & SIFT_F_SKIP_GAUSS_PLANES);
+  HIPCHK(ctx->dog.ensure((size_t)tot * P.ND * sizeof(float)));
+  if (keep_gauss) HIPCHK(ctx->gauss.ensure((size_t)tot * P.NS * sizeof(float)));
+  HIPCHK(ctx->seeds.ensure((size_t)std::max<long long>(1, tot - (long long)P.oct[0].h * P.oct[0].w) *
+                           sizeof(double)));
+  HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (img_host) {
+    HIPCHK(ctx->img.ensure((size_t)W * H * sizeof(float)));
+    HIPCHK(hipMemcpy2DAsync(ctx->img.p, W * sizeof(float), img_host, stride * sizeof(float),
+                            W * sizeof(float), H, hipMemcpyHostToDevice, ctx->stream));
+    P.img = ctx->img.as<float>();
+    P.img_stride = W;
+  } else {
+    P.img = img_dev;
+    P.img_stride = (int)stride;
+  }
+  P.seeds = ctx->seeds.as<double>();
+  P.dog = ctx->dog.as<float>();
+  HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  for (int o = 0; o < P.O; ++o) {
+    const Octave& oc = P.oct[o];
+    GaussLaunch L{};
+    L.o = o;
+    L.gauss = keep_gauss ? ctx->gauss.as<float>() + oc.gauss_off : nullptr;
+    L.dog = ctx->dog.as<float>() + oc.dog_off;
+    L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off : nullptr;
+    L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : 0;
+    L.base_lds = gauss_lds_bytes(oc, true) <= 112 * 1024 ? 1 : 0;
+    HIPCHK(launch_gauss_dog(P, L, ctx->stream));
+  }
+  HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  ctx->dog_source = kNative;
+  ctx->have_gauss = keep_gauss;
+  ctx->have_cand = false;
+  return SIFT_OK;
+}
+
+extern "C" {
+
+int sift_build_scale_space(sift_ctx* ctx, const float* img, int width, int height, size_t stride_px,
+                           const sift_params* p, const double* sig) {
+  int rc = build_common(ctx, img, nullptr, width, height, stride_px, p, sig);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  float a = 0, b = 0;
+  (void)hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
+  (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
+  ctx->tm.h2d_ms = a;
+  ctx->tm.gauss_dog_ms = b;
+  return SIFT_OK;
+}
+
+int sift_build_scale_space_device(sift_ctx* ctx, const float* d_img, int width, int height,
+                                  size_t stride_px, const sift_params* p, const double* sig) {
+  int rc = build_common(ctx, nullptr, d_img, width, height, stride_px, p, sig);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  float b = 0;
+  (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
+  ctx->tm.h2d_ms = 0;
+  ctx->tm.gauss_dog_ms = b;
+  return SIFT_OK;
+}
+
+int sift_get_dims(sift_ctx* ctx, int o, int* rows, int* cols) {
+  if (!ctx || !rows || !cols) return SIFT_E_ARG;
+  if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no pyramid");
+  if (o < 0 || o >= ctx->P.O) return set_err(ctx, SIFT_E_ARG, "octave out of range");
+  *rows = ctx->P.oct[o].h;
+  *cols = ctx->P.oct[o].w;
+  return SIFT_OK;
+}
+
+int sift_get_blur_level(sift_ctx* ctx, int kind, int o, int s, double* blur) {
+  if (!ctx || !blur) return SIFT_E_ARG;
+  if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no pyramid");
+  const int lim = kind == SIFT_PLANE_GAUSS ? ctx->P.NS : ctx->P.ND;
+  if (o < 0 || o >= ctx->P.O || s < 0 || s >= lim) return set_err(ctx, SIFT_E_ARG, "index out of range");
+  // DoG[s] carries L[s-1+1-1] = L[s].blurLevel (background.js:326-329).
+  *blur = ctx->blur[o * ctx->P.NS + s];
+  return SIFT_OK;
+}
+
+int sift_get_plane(sift_ctx* ctx, int kind, int o, int s, float* dst, size_t cap_px) {
+  if (!ctx || !dst) return SIFT_E_ARG;
+  if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no pyramid");
+  const Pyramid& P = ctx->P;
+  if (o < 0 || o >= P.O) return set_err(ctx, SIFT_E_ARG, "octave out of range");
+  const Octave& oc = P.oct[o];
+  const size_t plane = (size_t)oc.h * oc.w;
+  if (cap_px < plane) return set_err(ctx, SIFT_E_CAPACITY, "destination too small");
+  const float* src = nullptr;
+  if (kind == SIFT_PLANE_GAUSS) {
+    if (!ctx->have_gauss) return set_err(ctx, SIFT_E_STATE, "Gaussian planes not materialised");
+    if (s < 0 || s >= P.NS) return set_err(ctx, SIFT_E_ARG, "scale out of range");
+    src = ctx->gauss.as<float>() + oc.gauss_off + (size_t)s * plane;
+  } else if (kind == SIFT_PLANE_DOG) {
+    if (s < 0 || s >= P.ND) return set_err(ctx, SIFT_E_ARG, "scale out of range");
+    src = ctx->dog.as<float>() + oc.dog_off + (size_t)s * plane;
+  } else {
+    return set_err(ctx, SIFT_E_ARG, "bad plane kind");
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(dst, src, plane * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+int sift_load_dog(sift_ctx* ctx, const float* planes, int width, int height, const sift_params* p) {
+  if (!ctx || !planes) return SIFT_E_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = setup_geometry(ctx, width, height, p, nullptr, false);
+  if (rc) return rc;
+  const long long tot = total_plane_px(ctx);
+  HIPCHK(ctx->dog.ensure((size_t)tot * ctx->P.ND * sizeof(float)));
+  HIPCHK(hipMemcpyAsync(ctx->dog.p, planes, (size_t)tot * ctx->P.ND * sizeof(float),
+                        hipMemcpyHostToDevice, ctx->stream));
+  ctx->P.dog = ctx->dog.as<float>();
+  ctx->P.img = nullptr;
+  ctx->P.seeds = nullptr;
+  ctx->dog_source = kForeign;
+  ctx->have_gauss = false;
+  ctx->have_cand = false;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+int sift_load_scale_space(sift_ctx* ctx, const float* planes, int width, int height,
+                          const sift_params* p) {
+  if (!ctx || !planes) return SIFT_E_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = setup_geometry(ctx, width, height, p, nullptr, false);
+  if (rc) return rc;
+  const Pyramid& P = ctx->P;
+  const long long tot = total_plane_px(ctx);
+  HIPCHK(ctx->gauss.ensure((size_t)tot * P.NS * sizeof(float)));
+  HIPCHK(ctx->dog.ensure((size_t)tot * P.ND * sizeof(float)));
+  HIPCHK(hipMemcpyAsync(ctx->gauss.p, planes, (size_t)tot * P.NS * sizeof(float),
+                        hipMemcpyHostToDevice, ctx->stream));
+  for (int o = 0; o < P.O; ++o) {
+    const Octave& oc = P.oct[o];
+    HIPCHK(launch_dog_from_gauss(ctx->gauss.as<float>() + oc.gauss_off, ctx->dog.as<float>() + oc.dog_off,
+                                 (long long)oc.h * oc.w, P.ND, ctx->stream));
+  }
+  ctx->P.dog = ctx->dog.as<float>();
+  ctx->P.img = nullptr;
+  ctx->P.seeds = nullptr;
+  ctx->dog_source = kForeign;
+  ctx->have_gauss = true;
+  ctx->have_cand = false;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Extrema: scan -> sort by (octave, scale, y, x) -> exact tie resolution ->
+// ordered compaction.  Leaves ctx->cand_key / cand_val / n_cand.
+// ---------------------------------------------------------------------------
+static int run_extrema(sift_ctx* ctx) {
+  Pyramid& P = ctx->P;
+  const bool exact_planes = ctx->dog_source == kForeign;
+  unsigned* cnt = ctx->counters.as<unsigned>();
+  const long long tot = total_plane_px(ctx);
+  unsigned cap = (unsigned)std::min<long long>(0x7fffffffLL, std::max<long long>(4096, tot * P.S / 16));
+  if (ctx->ext_keys.bytes >= sizeof(unsigned) * 4096)
+    cap = std::max<unsigned>(cap, (unsigned)std::min<size_t>(0x7fffffff, ctx->ext_keys.bytes / sizeof(unsigned)));
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  unsigned n_emit = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    HIPCHK(ctx->ext_keys.ensure((size_t)cap * sizeof(unsigned)));
+    HIPCHK(ctx->ext_pay.ensure((size_t)cap * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), ctx->stream));
+    for (int o = 0; o < P.O; ++o) {
+      ExtremaLaunch L{};
+      L.o = o;
+      L.exact_planes = exact_planes;
+      L.keys = ctx->ext_keys.as<unsigned>();
+      L.payload = ctx->ext_pay.as<unsigned long long>();
+      L.counters = cnt;
+      L.cap = cap;
+      HIPCHK(launch_extrema(P, L, ctx->stream));
+    }
+    HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    n_emit = ctx->h_counters[0];
+    if (n_emit <= cap) break;
+    cap = n_emit + n_emit / 8 + 1024;
+  }
+  ctx->n_low = ctx->h_counters[1];
+  const int n = (int)n_emit;
+  // Sort records by key (the reference's octave/scale/raster order).
+  unsigned long long maxkey = 0;
+  for (int o = 0; o < P.O; ++o) maxkey = P.oct[o].key_off + (unsigned long long)P.S * P.oct[o].h * P.oct[o].w;
+  int end_bit = 1;
+  while (end_bit < 32 && (1ull << end_bit) <= maxkey) ++end_bit;
+  HIPCHK(ctx->srt_keys.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->srt_pay.ensure((size_t)std::max(n, 1) * sizeof(unsigned long long)));
+  HIPCHK(ctx->keep.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->pos.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->value.ensure((size_t)std::max(n, 1) * sizeof(double)));
+  HIPCHK(ctx->flagged.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->cand_key.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->cand_val.ensure((size_t)std::max(n, 1) * sizeof(double)));
+  ctx->n_exact = 0;
+  if (n > 0) {
+    size_t tb = 0, tb2 = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ctx->ext_keys.as<unsigned>(), ctx->srt_keys.as<unsigned>(),
+                                              ctx->ext_pay.as<unsigned long long>(),
+                                              ctx->srt_pay.as<unsigned long long>(), n, 0, end_bit, ctx->stream));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
+                                            ctx->stream));
+    HIPCHK(ctx->temp.ensure(std::max(tb, tb2)));
+    tb = ctx->temp.bytes;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->temp.p, tb, ctx->ext_keys.as<unsigned>(), ctx->srt_keys.as<unsigned>(),
+                                              ctx->ext_pay.as<unsigned long long>(),
+                                              ctx->srt_pay.as<unsigned long long>(), n, 0, end_bit, ctx->stream));
+    CandInit C{};
+    C.keys = ctx->srt_keys.as<unsigned>();
+    C.payload = ctx->srt_pay.as<unsigned long long>();
+    C.n = n;
+    C.keep = ctx->keep.as<unsigned>();
+    C.value = ctx->value.as<double>();
+    C.flagged = ctx->flagged.as<unsigned>();
+    C.counters = cnt;
+    HIPCHK(launch_cand_init(C, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_counters + 2, cnt + 2, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const unsigned nf = ctx->h_counters[2];
+    ctx->n_exact = nf;
+    if (nf) HIPCHK(launch_exact_extrema(P, C, nf, ctx->stream));
+    tb2 = ctx->temp.bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb2, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
+                                            ctx->stream));
+    HIPCHK(launch_scatter_candidates(ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), C.keys, C.value, n,
+                                     ctx->cand_key.as<unsigned>(), ctx->cand_val.as<double>(), ctx->stream));
+    unsigned last[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&last[0], ctx->pos.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(&last[1], ctx->keep.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_counters + 1, cnt + 1, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->n_cand = (size_t)last[0] + last[1];
+    ctx->n_low = ctx->h_counters[1];
+  } else {
+    ctx->n_cand = 0;
+  }
+  HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
+  ctx->have_cand = true;
+  return SIFT_OK;
+}
+
+static int run_refine(sift_ctx* ctx) {
+  Pyramid& P = ctx->P;
+  const int n = (int)ctx->n_cand;
+  unsigned* cnt = ctx->counters.as<unsigned>();
+  HIPCHK(hipEventRecord(ctx->ev[5], ctx->stream));
+  HIPCHK(ctx->status.ensure((size_t)std::max(n, 1) * sizeof(int)));
+  HIPCHK(ctx->kp_tmp.ensure((size_t)std::max(n, 1) * sizeof(Keypoint)));
+  HIPCHK(ctx->kp.ensure((size_t)std::max(n, 1) * sizeof(Keypoint)));
+  HIPCHK(ctx->uncertain.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->keep.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->pos.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
+  HIPCHK(hipMemsetAsync(cnt + 3, 0, 2 * sizeof(unsigned), ctx->stream));
+  ctx->n_kp = 0;
+  ctx->n_sing = 0;
+  if (n > 0) {
+    RefineLaunch R{};
+    R.cand_key = ctx->cand_key.as<unsigned>();
+    R.cand_val = ctx->cand_val.as<double>();
+    R.n = n;
+    R.exact_planes = ctx->dog_source == kForeign;
+    R.min_blur = ctx->p.min_blur;
+    R.min_interpixel_distance = ctx->p.min_interpixel_distance;
+    R.status = ctx->status.as<int>();
+    R.kp = ctx->kp_tmp.as<Keypoint>();
+    R.uncertain = ctx->uncertain.as<unsigned>();
+    R.counters = cnt;
+    HIPCHK(launch_refine_fast(P, R, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_counters + 3, cnt + 3, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const unsigned nu = ctx->h_counters[3];
+    ctx->n_exact += nu;
+    if (nu) {
+      if (ctx->dog_source != kNative) return set_err(ctx, SIFT_E_STATE, "uncertain refinement without a native pyramid");
+      HIPCHK(launch_refine_exact(P, R, nu, ctx->stream));
+    }
+    HIPCHK(launch_status_to_keep(R.status, ctx->keep.as<unsigned>(), n, ctx->stream));
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
+                                            ctx->stream));
+    HIPCHK(ctx->temp.ensure(tb));
+    tb = ctx->temp.bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
+                                            ctx->stream));
+    HIPCHK(launch_scatter_keypoints(R.status, ctx->pos.as<unsigned>(), R.kp, n, ctx->kp.as<Keypoint>(), ctx->stream));
+    unsigned last[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&last[0], ctx->pos.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(&last[1], ctx->keep.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_counters + 4, cnt + 4, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->n_kp = (size_t)last[0] + last[1];
+    ctx->n_sing = ctx->h_counters[4];
+  }
+  HIPCHK(hipEventRecord(ctx->ev[6], ctx->stream));
+  return SIFT_OK;
+}
+
+static void read_stage_times(sift_ctx* ctx, bool extrema, bool refine) {
+  float t = 0;
+  (void)hipEventSynchronize(ctx->ev[6]);
+  if (extrema && hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]) == hipSuccess) ctx->tm.extrema_ms = t;
+  if (refine && hipEventElapsedTime(&t, ctx->ev[5], ctx->ev[6]) == hipSuccess) ctx->tm.refine_ms = t;
+}
+
+extern "C" {
+
+int sift_copy_candidates(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->have_cand) return set_err(ctx, SIFT_E_STATE, "no candidates");
+  if (n_out) *n_out = ctx->n_cand;
+  if (!out) return SIFT_OK;
+  if (cap < ctx->n_cand) return set_err(ctx, SIFT_E_CAPACITY, "candidate buffer too small");
+  const size_t n = ctx->n_cand;
+  std::vector<unsigned> keys(n);
+  std::vector<double> vals(n);
+  if (n) {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(keys.data(), ctx->cand_key.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(vals.data(), ctx->cand_val.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  const Pyramid& P = ctx->P;
+  for (size_t i = 0; i < n; ++i) {
+    unsigned k = keys[i];
+    int o = 0;
+    while (o + 1 < P.O && k >= P.oct[o + 1].key_off) ++o;
+    unsigned r = k - P.oct[o].key_off;
+    const unsigned plane = (unsigned)P.oct[o].h * (unsigned)P.oct[o].w;
+    const int s = (int)(r / plane) + 1;
+    r -= (unsigned)(s - 1) * plane;
+    out[i].octave = o;
+    out[i].scale = s;
+    out[i].y = (int)(r / (unsigned)P.oct[o].w);
+    out[i].x = (int)(r % (unsigned)P.oct[o].w);
+    out[i].value = vals[i];
+  }
+  return SIFT_OK;
+}
+
+int sift_find_extrema(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* n_out, size_t* n_low) {
+  if (!ctx) return SIFT_E_ARG;
+  if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no DoG pyramid: build or load one first");
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = run_extrema(ctx);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(ctx->ev[6], ctx->stream));
+  read_stage_times(ctx, true, false);
+  if (n_low) *n_low = ctx->n_low;
+  return sift_copy_candidates(ctx, out, cap, n_out);
+}
+
+int sift_set_candidates(sift_ctx* ctx, const sift_extremum* cand, size_t n) {
+  if (!ctx || (!cand && n)) return SIFT_E_ARG;
+  if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no DoG pyramid");
+  const Pyramid& P = ctx->P;
+  std::vector<unsigned> keys(n);
+  std::vector<double> vals(n);
+  for (size_t i = 0; i < n; ++i) {
+    const sift_extremum& c = cand[i];
+    if (c.octave < 0 || c.octave >= P.O) return set_err(ctx, SIFT_E_ARG, "candidate octave out of range");
+    const Octave& oc = P.oct[c.octave];
+    if (c.scale < 1 || c.scale > P.S || c.y < 1 || c.y > oc.h - 2 || c.x < 1 || c.x > oc.w - 2)
+      return set_err(ctx, SIFT_E_ARG, "candidate outside the refinable interior");
+    keys[i] = oc.key_off + (unsigned)(c.scale - 1) * (unsigned)oc.h * (unsigned)oc.w + (unsigned)c.y * oc.w + c.x;
+    vals[i] = c.value;
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(ctx->cand_key.ensure(std::max<size_t>(n, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->cand_val.ensure(std::max<size_t>(n, 1) * sizeof(double)));
+  if (n) {
+    HIPCHK(hipMemcpyAsync(ctx->cand_key.p, keys.data(), n * sizeof(unsigned), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->cand_val.p, vals.data(), n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->n_cand = n;
+  ctx->have_cand = true;
+  return SIFT_OK;
+}
+
+int sift_copy_keypoints(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (n_out) *n_out = ctx->n_kp;
+  if (!out) return SIFT_OK;
+  if (cap < ctx->n_kp) return set_err(ctx, SIFT_E_CAPACITY, "keypoint buffer too small");
+  if (ctx->n_kp) {
+    HIPCHK(hipMemcpyAsync(out, ctx->kp.p, ctx->n_kp * sizeof(sift_keypoint), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  return SIFT_OK;
+}
+
+int sift_refine(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out, size_t* n_singular) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->have_cand) return set_err(ctx, SIFT_E_STATE, "no candidates: run sift_find_extrema first");
+  HIPCHK(hipSetDevice(ctx->device));
+  int rc = run_refine(ctx);
+  if (rc) return rc;
+  read_stage_times(ctx, false, true);
+  if (n_singular) *n_singular = ctx->n_sing;
+  rc = sift_copy_keypoints(ctx, out, cap, n_out);
+  if (rc) return rc;
+  if (ctx->n_sing) return set_err(ctx, SIFT_E_SINGULAR, "singular Hessian (the reference throws a TypeError here)");
+  return SIFT_OK;
+}
+
+static int detect_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
+                         size_t stride, const sift_params* p, sift_keypoint* out, size_t cap,
+                         size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr);
+  if (rc) return rc;
+  rc = run_extrema(ctx);
+  if (rc) return rc;
+  rc = run_refine(ctx);
+  if (rc) return rc;
+  float a = 0, b = 0;
+  (void)hipEventSynchronize(ctx->ev[6]);
+  if (img_host && hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->tm.h2d_ms = a;
+  if (!img_host) ctx->tm.h2d_ms = 0;
+  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]) == hipSuccess) ctx->tm.gauss_dog_ms = b;
+  read_stage_times(ctx, true, true);
+  rc = sift_copy_keypoints(ctx, out, cap, n_out);
+  if (rc) return rc;
+  if (ctx->n_sing) return set_err(ctx, SIFT_E_SINGULAR, "singular Hessian (the reference throws a TypeError here)");
+  return SIFT_OK;
+}
+
+int sift_detect(sift_ctx* ctx, const float* img, int width, int height, size_t stride_px, const sift_params* p,
+                sift_keypoint* out, size_t cap, size_t* n_out) {
+  if (ctx) (void)hipSetDevice(ctx->device);
+  return detect_common(ctx, img, nullptr, width, height, stride_px, p, out, cap, n_out);
+}
+
+int sift_detect_device(sift_ctx* ctx, const float* d_img, int width, int height, size_t stride_px,
+                       const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
+  if (ctx) (void)hipSetDevice(ctx->device);
+  return detect_common(ctx, nullptr, d_img, width, height, stride_px, p, out, cap, n_out);
+}
+
+int sift_last_counts(sift_ctx* ctx, size_t* nc, size_t* nl, size_t* nk, size_t* ns, size_t* ne) {
+  if (!ctx) return SIFT_E_ARG;
+  if (nc) *nc = ctx->n_cand;
+  if (nl) *nl = ctx->n_low;
+  if (nk) *nk = ctx->n_kp;
+  if (ns) *ns = ctx->n_sing;
+  if (ne) *ne = ctx->n_exact;
+  return SIFT_OK;
+}
+
+int sift_last_timings(sift_ctx* ctx, sift_timings* t) {
+  if (!ctx || !t) return SIFT_E_ARG;
+  *t = ctx->tm;
+  return SIFT_OK;
+}
+
+int sift_device_keypoints(sift_ctx* ctx, const sift_keypoint** d_kp, size_t* n) {
+  if (!ctx || !d_kp || !n) return SIFT_E_ARG;
+  *d_kp = ctx->kp.as<const sift_keypoint>();
+  *n = ctx->n_kp;
+  return SIFT_OK;
+}
+
+}  // extern "C"

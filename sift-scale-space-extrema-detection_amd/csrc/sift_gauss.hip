@@ -1,0 +1,160 @@
+// Gaussian scale space + Difference-of-Gaussians for one octave (gfx950).
+//
+// Replaces background.js:71-237 (computeGaussianScaleSpace, whose hot loop is
+// SIFT_blurMatrix2DChunk, sift.js:72-149) and background.js:258-354
+// (computeDifferenceOfGaussians / SIFT_subtractMatrix2DChunk, sift.js:154-188).
+//
+// The reference convolves every scale of an octave with a full 2D kernel of
+// the SAME octave base (the blur is not incremental, background.js:173-177).
+// Here each 64x32 output tile stages that base once (replicated-edge region
+// in LDS, fp64), then for every scale runs the separable form of the same
+// kernel -- a horizontal pass into an fp64 LDS strip and a vertical pass with
+// an 8-row register sliding window -- and writes L_s (fp32), the DoG
+// L_{s-1} - L_s formed in fp64 and rounded once (fp32), and for s == S the
+// fp64 subsample that seeds the next octave (background.js:114-118).
+//
+// Roofline: HBM-bound on the plane stores.  Per octave pixel the kernel
+// writes 4(S+3) + 4(S+2) bytes (+8/4 for the seed) and reads 1 (octave 0:
+// 4 bytes per 4 pixels) or 8/4 bytes of base.  fp64 VALU work per pixel is
+// sum_s 2(2r_s+1) FMAs; it overlaps the store stream.
+#include "sift_common.h"
+#include "sift_kernels.h"
+
+namespace sift {
+
+template <bool BASE_LDS>
+__global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Octave& oc = P.oct[L.o];
+  const int h = oc.h, w = oc.w, R = oc.rmax;
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+  const int tid = threadIdx.x, lane = tid & 63, ty = (tid >> 6) * kVT;
+  const double* __restrict__ wts = P.wts;
+
+  // Rows this tile can touch, clamped: the strip only holds distinct rows.
+  const int lo_all = max(0, y0 - R), hi_all = min(h - 1, y0 + kTY - 1 + R);
+  const int BW = kTX + 2 * R;
+  double* sH = smem;
+  double* sB = smem + (size_t)(hi_all - lo_all + 1) * kTX;
+
+  if (BASE_LDS) {
+    // Replicated-edge base region: rows y0-R .. y0+kTY+R-1 restricted to the
+    // clamped range, columns x0-R .. x0+kTX+R-1 with clamped sources.
+    const int nr = hi_all - lo_all + 1;
+    for (int idx = tid; idx < nr * BW; idx += 256) {
+      const int rr = idx / BW, cc = idx - rr * BW;
+      const int x = clampi(x0 - R + cc, 0, w - 1);
+      sB[idx] = base_at(P, L.o, lo_all + rr, x);
+    }
+    __syncthreads();
+  }
+
+  const long long plane = (long long)h * w;
+  const int x = x0 + lane;
+  double lprev[kVT];
+#pragma unroll
+  for (int t = 0; t < kVT; ++t) lprev[t] = 0.0;
+
+  for (int s = 0; s < P.NS; ++s) {
+    const int r = oc.rad[s];
+    const double* __restrict__ wp = wts + oc.wofs[s];
+    const int lo = max(0, y0 - r), hi = min(h - 1, y0 + kTY - 1 + r);
+    const int nrows = hi - lo + 1;
+
+    // Horizontal pass: sH[y - lo][c] = sum_i w_i * B(y, clamp(x0 + c - r + i)).
+    for (int idx = tid; idx < nrows * kTX; idx += 256) {
+      const int rr = idx >> 6, c = idx & 63;
+      const int y = lo + rr;
+      double acc = 0.0;
+      if (BASE_LDS) {
+        const double* row = sB + (size_t)(y - lo_all) * BW + (c + R - r);
+        for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], row[i], acc);
+      } else {
+        const int xb = x0 + c - r;
+        for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], base_at(P, L.o, y, clampi(xb + i, 0, w - 1)), acc);
+      }
+      sH[idx] = acc;
+    }
+    __syncthreads();
+
+    // Vertical pass, 8 outputs per thread: output row y0+ty+t reads strip
+    // rows clamp(y0+ty+t-r+k), k = 0..2r.  Zero-padded taps keep the fma
+    // sequence identical to a plain k = 0..2r sum for every t.
+    double acc[kVT];
+#pragma unroll
+    for (int t = 0; t < kVT; ++t) acc[t] = 0.0;
+    for (int j = 0; j < 2 * r + kVT; ++j) {
+      const int yy = clampi(y0 + ty - r + j, 0, h - 1) - lo;
+      const double v = sH[yy * kTX + lane];
+#pragma unroll
+      for (int t = 0; t < kVT; ++t) acc[t] = fma(wp[j - t], v, acc[t]);
+    }
+    __syncthreads();  // the strip is rewritten by the next scale
+
+    if (x < w) {
+#pragma unroll
+      for (int t = 0; t < kVT; ++t) {
+        const int y = y0 + ty + t;
+        if (y < h) {
+          const long long p = (long long)y * w + x;
+          if (L.gauss) L.gauss[s * plane + p] = (float)acc[t];
+          if (s > 0) L.dog[(s - 1) * plane + p] = (float)(lprev[t] - acc[t]);
+          if (s == P.S && L.next_seed && !(y & 1) && !(x & 1))
+            L.next_seed[(long long)(y >> 1) * L.next_w + (x >> 1)] = acc[t];
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < kVT; ++t) lprev[t] = acc[t];
+  }
+}
+
+// DoG from a caller-supplied fp32 Gaussian pyramid (foreign scale space):
+// D[t] = L[t] - L[t+1] in fp64 (exact for fp32 operands), rounded once.
+__global__ __launch_bounds__(256) void k_dog_from_gauss(const float* __restrict__ g,
+                                                        float* __restrict__ d, long long plane,
+                                                        int nd) {
+  const long long n = plane * nd;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    d[i] = (float)((double)g[i] - (double)g[i + plane]);
+  }
+}
+
+size_t gauss_lds_bytes(const Octave& oc, bool base_lds) {
+  const int R = oc.rmax;
+  const int rows = std::min(oc.h, kTY + 2 * R);
+  size_t b = (size_t)rows * kTX * sizeof(double);
+  if (base_lds) b += (size_t)rows * (kTX + 2 * R) * sizeof(double);
+  return b;
+}
+
+hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t st) {
+  const Octave& oc = P.oct[L.o];
+  dim3 grid((oc.w + kTX - 1) / kTX, (oc.h + kTY - 1) / kTY);
+  const size_t lds = gauss_lds_bytes(oc, L.base_lds);
+  static bool attr_set = false;
+  if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+    (void)hipFuncSetAttribute((const void*)k_gauss_dog<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_gauss_dog<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  if (L.base_lds) {
+    hipLaunchKernelGGL(k_gauss_dog<true>, grid, dim3(256), lds, st, P, L);
+  } else {
+    hipLaunchKernelGGL(k_gauss_dog<false>, grid, dim3(256), lds, st, P, L);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd,
+                                 hipStream_t st) {
+  long long n = plane * nd;
+  int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_dog_from_gauss, dim3(blocks), dim3(256), 0, st, g, d, plane, nd);
+  return hipGetLastError();
+}
+
+}  // namespace sift

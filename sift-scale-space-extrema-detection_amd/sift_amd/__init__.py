@@ -1,0 +1,340 @@
+"""Python binding of libsift_hip.so (the C ABI in include/sift_hip.h).
+
+This is host plumbing for tests, the bench and Python callers; the Node
+N-API addon (../napi) binds the same symbols for the JS drop-in.  There is
+no CPU fallback: if the HIP library is missing, import of the binding fails
+loudly (SiftLibraryError) -- the CPU oracle lives in /oracle and is test
+infrastructure only.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libsift_hip.so")
+
+SIFT_OK = 0
+SIFT_E_ARG = -1
+SIFT_E_HIP = -2
+SIFT_E_CAPACITY = -3
+SIFT_E_STATE = -4
+SIFT_E_SINGULAR = -5
+SIFT_E_UNSUPPORTED = -6
+
+PLANE_GAUSS = 0
+PLANE_DOG = 1
+
+F_SKIP_GAUSS_PLANES = 1
+
+# Exported symbols, exactly those include/sift_hip.h declares.
+ABI_SYMBOLS = (
+    "sift_abi_version", "sift_params_default", "sift_ctx_create", "sift_ctx_destroy",
+    "sift_last_error", "sift_schedule", "sift_octave_dims", "sift_build_scale_space",
+    "sift_build_scale_space_device", "sift_get_dims", "sift_get_blur_level", "sift_get_plane",
+    "sift_load_dog", "sift_load_scale_space", "sift_find_extrema", "sift_refine",
+    "sift_set_candidates", "sift_copy_candidates", "sift_copy_keypoints", "sift_detect", "sift_detect_device", "sift_last_counts",
+    "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
+)
+
+
+class SiftLibraryError(RuntimeError):
+    pass
+
+
+class SiftError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("sift error %d: %s" % (code, msg))
+        self.code = code
+
+
+class SiftSingularError(SiftError):
+    """The reference throws a TypeError here (matrix2d.js:482 -> :455)."""
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("num_octaves", ctypes.c_int), ("scales_per_octave", ctypes.c_int),
+                ("min_blur", ctypes.c_double), ("assumed_blur", ctypes.c_double),
+                ("min_interpixel_distance", ctypes.c_double), ("flags", ctypes.c_int)]
+
+
+class Extremum(ctypes.Structure):
+    _fields_ = [("octave", ctypes.c_int32), ("scale", ctypes.c_int32), ("x", ctypes.c_int32),
+                ("y", ctypes.c_int32), ("value", ctypes.c_double)]
+
+
+class Keypoint(ctypes.Structure):
+    _fields_ = [("octave", ctypes.c_int32), ("scale_level", ctypes.c_int32),
+                ("local_x", ctypes.c_int32), ("local_y", ctypes.c_int32),
+                ("abs_x", ctypes.c_double), ("abs_y", ctypes.c_double),
+                ("abs_sigma", ctypes.c_double), ("interp_value", ctypes.c_double)]
+
+
+class Timings(ctypes.Structure):
+    _fields_ = [("gauss_dog_ms", ctypes.c_double), ("extrema_ms", ctypes.c_double),
+                ("refine_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double)]
+
+
+EXTREMUM_DTYPE = np.dtype([("octave", "<i4"), ("scale", "<i4"), ("x", "<i4"), ("y", "<i4"),
+                           ("value", "<f8")])
+KEYPOINT_DTYPE = np.dtype([("octave", "<i4"), ("scale_level", "<i4"), ("local_x", "<i4"),
+                           ("local_y", "<i4"), ("abs_x", "<f8"), ("abs_y", "<f8"),
+                           ("abs_sigma", "<f8"), ("interp_value", "<f8")])
+
+_lib = None
+
+
+def lib():
+    """Load libsift_hip.so (raises SiftLibraryError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SiftLibraryError("libsift_hip.so not built: run `make lib` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    sz = ctypes.c_size_t
+    szp = ctypes.POINTER(ctypes.c_size_t)
+    dp = ctypes.POINTER(ctypes.c_double)
+    ip = ctypes.POINTER(ctypes.c_int)
+    fp = ctypes.POINTER(ctypes.c_float)
+    pp = ctypes.POINTER(Params)
+    sig = {
+        "sift_abi_version": (ctypes.c_int, []),
+        "sift_params_default": (ctypes.c_int, [pp]),
+        "sift_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+        "sift_ctx_destroy": (ctypes.c_int, [vp]),
+        "sift_last_error": (ctypes.c_char_p, [vp]),
+        "sift_schedule": (ctypes.c_int, [pp, dp, dp]),
+        "sift_octave_dims": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ip]),
+        "sift_build_scale_space": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, sz, pp, dp]),
+        "sift_build_scale_space_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, dp]),
+        "sift_get_dims": (ctypes.c_int, [vp, ctypes.c_int, ip, ip]),
+        "sift_get_blur_level": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, dp]),
+        "sift_get_plane": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp, sz]),
+        "sift_load_dog": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, pp]),
+        "sift_load_scale_space": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, pp]),
+        "sift_find_extrema": (ctypes.c_int, [vp, vp, sz, szp, szp]),
+        "sift_refine": (ctypes.c_int, [vp, vp, sz, szp, szp]),
+        "sift_set_candidates": (ctypes.c_int, [vp, vp, sz]),
+        "sift_copy_candidates": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_copy_keypoints": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_detect": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
+        "sift_detect_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
+        "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
+        "sift_last_timings": (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
+        "sift_device_keypoints": (ctypes.c_int, [vp, ctypes.POINTER(vp), szp]),
+        "sift_stream": (vp, [vp]),
+        "sift_synchronize": (ctypes.c_int, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def make_params(num_octaves=5, scales_per_octave=3, min_blur=0.8, assumed_blur=0.5,
+                min_interpixel_distance=0.5, flags=0):
+    """Defaults follow src/worker.js:29-98."""
+    return Params(int(num_octaves), int(scales_per_octave), float(min_blur), float(assumed_blur),
+                  float(min_interpixel_distance), int(flags))
+
+
+def schedule(params):
+    O, NS = params.num_octaves, params.scales_per_octave + 3
+    blur = np.zeros(O * NS)
+    sig = np.zeros(O * NS)
+    rc = lib().sift_schedule(ctypes.byref(params), blur.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                             sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if rc:
+        raise SiftError(rc, "sift_schedule")
+    return blur.reshape(O, NS), sig.reshape(O, NS)
+
+
+def octave_dims(width, height, num_octaves):
+    d = np.zeros(2 * num_octaves, dtype=np.int32)
+    rc = lib().sift_octave_dims(int(width), int(height), int(num_octaves),
+                                d.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    if rc:
+        raise SiftError(rc, "sift_octave_dims")
+    return [(int(d[2 * o]), int(d[2 * o + 1])) for o in range(num_octaves)]
+
+
+class Context:
+    """One sift_ctx: a HIP stream plus device-resident pyramids on `device`."""
+
+    def __init__(self, device=0):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        rc = self._L.sift_ctx_create(int(device), ctypes.byref(h))
+        if rc:
+            raise SiftError(rc, "sift_ctx_create(device=%d) failed (no HIP device?)" % device)
+        self._h = h
+        self.params = None
+        self.width = self.height = 0
+
+    def close(self):
+        if self._h:
+            self._L.sift_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc == SIFT_OK:
+            return
+        msg = "%s: %s" % (what, self._L.sift_last_error(self._h).decode())
+        if rc == SIFT_E_SINGULAR:
+            raise SiftSingularError(rc, msg)
+        raise SiftError(rc, msg)
+
+    # -- stages -----------------------------------------------------------
+    def build_scale_space(self, img, params, offset_sigmas=None):
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        H, W = img.shape
+        sig = None
+        if offset_sigmas is not None:
+            sig = np.ascontiguousarray(offset_sigmas, dtype=np.float64).ravel()
+            sig = sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        rc = self._L.sift_build_scale_space(self._h, img.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                            W, H, W, ctypes.byref(params), sig)
+        self._check(rc, "sift_build_scale_space")
+        self.params, self.width, self.height = params, W, H
+
+    def build_scale_space_device(self, d_ptr, width, height, params, stride=None):
+        rc = self._L.sift_build_scale_space_device(self._h, ctypes.c_void_p(int(d_ptr)), int(width),
+                                                   int(height), int(stride or width),
+                                                   ctypes.byref(params), None)
+        self._check(rc, "sift_build_scale_space_device")
+        self.params, self.width, self.height = params, width, height
+
+    def dims(self, octave):
+        r, c = ctypes.c_int(), ctypes.c_int()
+        self._check(self._L.sift_get_dims(self._h, octave, ctypes.byref(r), ctypes.byref(c)), "sift_get_dims")
+        return r.value, c.value
+
+    def blur_level(self, kind, octave, scale):
+        b = ctypes.c_double()
+        self._check(self._L.sift_get_blur_level(self._h, kind, octave, scale, ctypes.byref(b)),
+                    "sift_get_blur_level")
+        return b.value
+
+    def plane(self, kind, octave, scale):
+        h, w = self.dims(octave)
+        out = np.empty((h, w), dtype=np.float32)
+        self._check(self._L.sift_get_plane(self._h, kind, octave, scale,
+                                           out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), h * w),
+                    "sift_get_plane")
+        return out
+
+    def load_dog(self, planes_flat, width, height, params):
+        a = np.ascontiguousarray(planes_flat, dtype=np.float32)
+        self._check(self._L.sift_load_dog(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                          int(width), int(height), ctypes.byref(params)), "sift_load_dog")
+        self.params, self.width, self.height = params, width, height
+
+    def load_scale_space(self, planes_flat, width, height, params):
+        a = np.ascontiguousarray(planes_flat, dtype=np.float32)
+        self._check(self._L.sift_load_scale_space(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                  int(width), int(height), ctypes.byref(params)),
+                    "sift_load_scale_space")
+        self.params, self.width, self.height = params, width, height
+
+    def find_extrema(self):
+        n, low = ctypes.c_size_t(), ctypes.c_size_t()
+        self._check(self._L.sift_find_extrema(self._h, None, 0, ctypes.byref(n), ctypes.byref(low)),
+                    "sift_find_extrema")
+        return self.candidates(), int(low.value)
+
+    def candidates(self):
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_copy_candidates(self._h, None, 0, ctypes.byref(n)), "sift_copy_candidates")
+        out = np.zeros(max(n.value, 1), dtype=EXTREMUM_DTYPE)
+        self._check(self._L.sift_copy_candidates(self._h, out.ctypes.data_as(ctypes.c_void_p), out.shape[0],
+                                                 ctypes.byref(n)), "sift_copy_candidates")
+        return out[:n.value]
+
+    def keypoints(self):
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_copy_keypoints(self._h, None, 0, ctypes.byref(n)), "sift_copy_keypoints")
+        out = np.zeros(max(n.value, 1), dtype=KEYPOINT_DTYPE)
+        self._check(self._L.sift_copy_keypoints(self._h, out.ctypes.data_as(ctypes.c_void_p), out.shape[0],
+                                                ctypes.byref(n)), "sift_copy_keypoints")
+        return out[:n.value]
+
+    def set_candidates(self, cand):
+        c = np.ascontiguousarray(cand, dtype=EXTREMUM_DTYPE)
+        self._check(self._L.sift_set_candidates(self._h, c.ctypes.data_as(ctypes.c_void_p), c.shape[0]),
+                    "sift_set_candidates")
+
+    def refine(self, raise_singular=False):
+        n, ns = ctypes.c_size_t(), ctypes.c_size_t()
+        rc = self._L.sift_refine(self._h, None, 0, ctypes.byref(n), ctypes.byref(ns))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_refine")
+        return self.keypoints(), int(ns.value)
+
+    def detect(self, img, params, raise_singular=False):
+        img = np.ascontiguousarray(img, dtype=np.float32)
+        H, W = img.shape
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect(self._h, img.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), W, H, W,
+                                 ctypes.byref(params), None, 0, ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect")
+        self.params, self.width, self.height = params, W, H
+        return self.keypoints()
+
+    def detect_device(self, d_ptr, width, height, params, stride=None, raise_singular=False):
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect_device(self._h, ctypes.c_void_p(int(d_ptr)), int(width), int(height),
+                                        int(stride or width), ctypes.byref(params), None, 0, ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect_device")
+        self.params, self.width, self.height = params, width, height
+        return n.value
+
+    def device_keypoints(self):
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(self._L.sift_device_keypoints(self._h, ctypes.byref(p), ctypes.byref(n)),
+                    "sift_device_keypoints")
+        return p.value or 0, n.value
+
+    def counts(self):
+        v = [ctypes.c_size_t() for _ in range(5)]
+        self._check(self._L.sift_last_counts(self._h, *[ctypes.byref(x) for x in v]), "sift_last_counts")
+        keys = ("candidates", "low_contrast", "keypoints", "singular", "exact")
+        return dict(zip(keys, (x.value for x in v)))
+
+    def timings(self):
+        t = Timings()
+        self._check(self._L.sift_last_timings(self._h, ctypes.byref(t)), "sift_last_timings")
+        return dict(gauss_dog_ms=t.gauss_dog_ms, extrema_ms=t.extrema_ms, refine_ms=t.refine_ms,
+                    h2d_ms=t.h2d_ms)
+
+    def stream(self):
+        return self._L.sift_stream(self._h)
+
+    def synchronize(self):
+        self._check(self._L.sift_synchronize(self._h), "sift_synchronize")
+
+
+def flatten_pyramid(planes):
+    """[[2D arrays per scale] per octave] -> flat fp32 octave-major buffer."""
+    return np.concatenate([np.asarray(p, dtype=np.float32).ravel() for octv in planes for p in octv])

@@ -1,0 +1,194 @@
+"""Parity of the HIP path (through the C ABI) with the reference.
+
+* golden cases: against vectors the reference itself produced
+  (tests/golden), for the one-call path and the stage-by-stage path;
+* larger sizes: against the pinned CPU oracle (fp64 C restatement);
+* caller-supplied pyramids (sift_load_dog / sift_load_scale_space): exact
+  against the oracle run on the same fp32 planes;
+* quirks and edge cases the reference has (singular Hessian, flat images,
+  tiny octaves), determinism.
+
+Tolerances: keypoint (x, y, sigma) within 1e-4 (BASELINE.json north_star),
+identical candidate / keypoint sets and order, plane values within fp32
+rounding of the reference's fp64 values.
+"""
+import numpy as np
+import pytest
+
+import oracle as orc
+import sift_amd
+from golden_util import Golden, case_names
+from sift_amd.synth import blob_image
+
+pytestmark = pytest.mark.gpu
+
+XY_SIGMA_TOL = 1e-4
+
+
+def params_of(g, flags=0):
+    P = g.params
+    return sift_amd.make_params(P["num_octaves"], P["scales_per_octave"], P["min_blur"], P["assumed_blur"],
+                                P["min_interpixel_distance"], flags)
+
+
+def check_candidates(c, ref, value_rtol=2 ** -23):
+    """c: EXTREMUM_DTYPE array; ref: (N,5) [o, s, x, y, value]."""
+    assert c.shape[0] == ref.shape[0], (c.shape[0], ref.shape[0])
+    got = np.stack([c["octave"], c["scale"], c["x"], c["y"]], axis=1)
+    np.testing.assert_array_equal(got, ref[:, :4].astype(np.int64))
+    np.testing.assert_allclose(c["value"], ref[:, 4], rtol=value_rtol, atol=1e-15)
+
+
+def check_keypoints(k, ref):
+    """k: KEYPOINT_DTYPE array; ref: (M,8) reference order."""
+    assert k.shape[0] == ref.shape[0], (k.shape[0], ref.shape[0])
+    ints = np.stack([k["octave"], k["scale_level"], k["local_x"], k["local_y"]], axis=1)
+    np.testing.assert_array_equal(ints, ref[:, :4].astype(np.int64))
+    np.testing.assert_allclose(k["abs_sigma"], ref[:, 4], rtol=0, atol=XY_SIGMA_TOL)
+    np.testing.assert_allclose(k["abs_x"], ref[:, 5], rtol=0, atol=XY_SIGMA_TOL)
+    np.testing.assert_allclose(k["abs_y"], ref[:, 6], rtol=0, atol=XY_SIGMA_TOL)
+    np.testing.assert_allclose(k["interp_value"], ref[:, 7], rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_detect_matches_reference(gpu_ctx, name):
+    g = Golden(name)
+    kp = gpu_ctx.detect(g.img, params_of(g))
+    check_candidates(gpu_ctx.candidates(), g.candidates)
+    check_keypoints(kp, g.refined)
+    cnt = gpu_ctx.counts()
+    assert cnt["low_contrast"] == int(g.z["low_contrast_counts"].sum())
+    assert cnt["singular"] == 0
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_stage_api_matches_reference(gpu_ctx, name):
+    """computeGaussianScaleSpace -> computeDifferenceOfGaussians ->
+    findCandidateKeypoints -> refineCandidateKeypoints, stage by stage."""
+    g = Golden(name)
+    p = params_of(g)
+    gpu_ctx.build_scale_space(g.img, p)
+    z = g.z
+    O, S = p.num_octaves, p.scales_per_octave
+    for o in range(O):
+        assert gpu_ctx.dims(o) == tuple(z["dims"][o])
+        pos = z["sample_pos"][o]
+        for s in range(S + 3):
+            L = gpu_ctx.plane(sift_amd.PLANE_GAUSS, o, s).astype(np.float64)
+            ref = z["gauss_samples"][o][s]
+            np.testing.assert_allclose(L[pos[:, 0], pos[:, 1]], ref, rtol=2 ** -24, atol=1e-13)
+            assert gpu_ctx.blur_level(sift_amd.PLANE_GAUSS, o, s) == pytest.approx(z["gauss_blur"][o][s], rel=1e-15)
+        for s in range(S + 2):
+            D = gpu_ctx.plane(sift_amd.PLANE_DOG, o, s).astype(np.float64)
+            ref = z["dog_samples"][o][s]
+            np.testing.assert_allclose(D[pos[:, 0], pos[:, 1]], ref, rtol=2 ** -24, atol=1e-13)
+    cand, low = gpu_ctx.find_extrema()
+    check_candidates(cand, g.candidates)
+    assert low == int(z["low_contrast_counts"].sum())
+    kp, sing = gpu_ctx.refine()
+    check_keypoints(kp, g.refined)
+    assert sing == 0
+
+
+def _oracle_params(p):
+    return orc.make_params(p.num_octaves, p.scales_per_octave, p.min_blur, p.assumed_blur,
+                           p.min_interpixel_distance)
+
+
+@pytest.mark.parametrize("W,H,O,S,seed", [(1920, 1080, 4, 5, 11), (640, 480, 5, 3, 12), (333, 517, 4, 4, 13)])
+def test_detect_matches_oracle_large(gpu_ctx, W, H, O, S, seed):
+    img = blob_image(W, H, seed=seed)
+    p = sift_amd.make_params(O, S)
+    kp = gpu_ctx.detect(img, p)
+    r = orc.OracleRun(img, _oracle_params(p), orc.CONV_SEPARABLE)
+    check_candidates(gpu_ctx.candidates(), r.candidates())
+    check_keypoints(kp, r.refined)
+    assert gpu_ctx.counts()["low_contrast"] == r.n_low
+
+
+def test_foreign_dog_is_exact(gpu_ctx):
+    """findCandidateKeypoints / refineCandidateKeypoints on a DoG pyramid the
+    context did not build: the fp32 planes are the data, results are exact."""
+    img = blob_image(200, 150, seed=21)
+    p = sift_amd.make_params(4, 3)
+    op = _oracle_params(p)
+    r = orc.OracleRun(img, op, orc.CONV_SEPARABLE)
+    dog32 = r.dog_flat.astype(np.float32)
+    gpu_ctx.load_dog(dog32, 200, 150, p)
+    cand, low = gpu_ctx.find_extrema()
+    # oracle on the same fp32 values
+    r.dog_flat = dog32.astype(np.float64)
+    import ctypes
+    lowc = ctypes.c_long(0)
+    L = orc.lib()
+    n = L.oracle_find_extrema(ctypes.byref(op), 200, 150, r.dog_flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                              None, None, 0, ctypes.byref(lowc))
+    rec = np.zeros((max(n, 1), 4), dtype=np.int32)
+    val = np.zeros(max(n, 1))
+    L.oracle_find_extrema(ctypes.byref(op), 200, 150, r.dog_flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                          rec.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                          val.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n, ctypes.byref(lowc))
+    ref = np.concatenate([rec[:n], val[:n, None]], axis=1).astype(np.float64)
+    check_candidates(cand, ref, value_rtol=0)
+    assert low == lowc.value
+    kp, sing = gpu_ctx.refine()
+    out, osing = r.refine(rec[:n], val[:n])
+    assert sing == osing
+    assert kp.shape[0] == out.shape[0]
+    got = np.stack([kp["abs_sigma"], kp["abs_x"], kp["abs_y"], kp["interp_value"]], axis=1)
+    np.testing.assert_allclose(got, out[:, 4:], rtol=1e-14, atol=1e-15)
+
+
+def test_foreign_scale_space_dog(gpu_ctx):
+    """computeDifferenceOfGaussians on a caller scale space: D = L[s-1]-L[s]."""
+    img = blob_image(96, 80, seed=22)
+    p = sift_amd.make_params(3, 3)
+    r = orc.OracleRun(img, _oracle_params(p), orc.CONV_SEPARABLE)
+    g32 = r.gauss_flat.astype(np.float32)
+    gpu_ctx.load_scale_space(g32, 96, 80, p)
+    off = 0
+    for o, (h, w) in enumerate(r.dims):
+        G = g32[off:off + 6 * h * w].reshape(6, h, w).astype(np.float64)
+        off += 6 * h * w
+        for s in range(5):
+            D = gpu_ctx.plane(sift_amd.PLANE_DOG, o, s)
+            np.testing.assert_array_equal(D, (G[s] - G[s + 1]).astype(np.float32))
+
+
+def test_singular_hessian_is_reported(gpu_ctx):
+    """Flat DoG around a candidate: det(H) = 0 -> the reference throws a
+    TypeError (matrix2d.js:482 -> :455); the ABI returns SIFT_E_SINGULAR."""
+    p = sift_amd.make_params(2, 3)
+    dims = sift_amd.octave_dims(16, 16, 2)
+    total = sum(h * w for h, w in dims) * 5
+    gpu_ctx.load_dog(np.zeros(total, dtype=np.float32), 16, 16, p)
+    cand = np.zeros(1, dtype=sift_amd.EXTREMUM_DTYPE)
+    cand[0] = (0, 1, 5, 5, 0.0)
+    gpu_ctx.set_candidates(cand)
+    with pytest.raises(sift_amd.SiftSingularError):
+        gpu_ctx.refine(raise_singular=True)
+    kp, sing = gpu_ctx.refine()
+    assert kp.shape[0] == 0 and sing == 1
+
+
+def test_flat_image_has_no_keypoints(gpu_ctx):
+    img = np.full((64, 48), 0.25, dtype=np.float32)
+    kp = gpu_ctx.detect(img, sift_amd.make_params(4, 3))
+    assert kp.shape[0] == 0 and gpu_ctx.counts()["candidates"] == 0
+
+
+def test_detect_is_deterministic(gpu_ctx):
+    img = blob_image(512, 384, seed=23)
+    p = sift_amd.make_params(4, 5)
+    a = gpu_ctx.detect(img, p)
+    b = gpu_ctx.detect(img, p)
+    assert a.tobytes() == b.tobytes()
+
+
+def test_skip_gauss_planes_same_keypoints(gpu_ctx):
+    img = blob_image(300, 200, seed=24)
+    a = gpu_ctx.detect(img, sift_amd.make_params(4, 4))
+    b = gpu_ctx.detect(img, sift_amd.make_params(4, 4, flags=sift_amd.F_SKIP_GAUSS_PLANES))
+    assert a.tobytes() == b.tobytes()
+    with pytest.raises(sift_amd.SiftError):
+        gpu_ctx.plane(sift_amd.PLANE_GAUSS, 0, 0)
