@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X SIFT scale-space extrema path.
+
+One step = one pass of the hot path over one synthetic image per GPU:
+Gaussian scale space + DoG (k_gauss_dog), 26-neighbour extrema scan with
+ordering and exact tie resolution, quadratic refinement -- all through the
+C ABI (sift_detect_device, input already resident in HBM).  With N > 1 GPUs
+(one process per GPU, torchrun), every rank processes its own image and the
+keypoint lists are all-gathered over RCCL (xGMI) each step: weak scaling.
+
+Prints ONE JSON line (rank 0).  Workload defaults to BASELINE.json's metric
+configuration: 3840x2160 (4K), 4 octaves x 5 scales.
+
+Roofline of the dominant kernel (k_gauss_dog, HBM-bound): algorithmic bytes
+B_alg = 4WH + sum_o 4 P_o (S+3) + sum_o 4 P_o (S+2) (input
+read + Gaussian and DoG planes written, fp32), divided by the kernel's
+HIP-event time on the context's stream.  `traffic` comes from the committed
+rocprofv3 PMC summary (profiles/*pmc*.json) when it matches the config.
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sift-scale-space-extrema-detection_amd"))
+
+METRIC = "Mpix/s through Gaussian+DoG+extrema, 4K img, 4 oct × 5 scales; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def octave_dims(W, H, O):
+    h, w, out = 2 * H, 2 * W, []
+    for o in range(O):
+        if o:
+            h, w = (h + 1) // 2, (w + 1) // 2
+        out.append((h, w))
+    return out
+
+
+def alg_bytes(W, H, O, S, skip_gauss):
+    P = [h * w for h, w in octave_dims(W, H, O)]
+    b = 4 * W * H + sum(4 * p * (S + 2) for p in P)
+    if skip_gauss:
+        b += sum(8 * p for p in P[1:])  # fp64 seeds written instead of the Gaussian planes
+    else:
+        b += sum(4 * p * (S + 3) for p in P)
+    return b
+
+
+def load_traffic(cfg_key):
+    """Per-launch HBM bytes of k_gauss_dog from a committed PMC summary."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_launch"):
+            return float(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
+def cpu_baseline(img_full, O, S, sample_w, sample_h):
+    """The oracle's reference-faithful 2D-kernel port, 1 thread, on a crop."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    crop = img_full[:sample_h, :sample_w].copy()
+    p = orc.make_params(O, S)
+    t0 = time.perf_counter()
+    nk, nc = orc.detect_count(crop, p, orc.CONV_2D)
+    dt = time.perf_counter() - t0
+    return {"value": round(sample_w * sample_h / dt / 1e6, 6), "unit": "Mpix/s", "cores": 1, "kind": "port",
+            "sample": "%dx%d crop of the same synthetic image, %d oct x %d scales, G+DoG+extrema+refine, "
+                      "reference 2D-kernel algorithm restated in C (oracle/sift_oracle.c CONV_2D), "
+                      "%.1f s, %d keypoints" % (sample_w, sample_h, O, S, dt, nk)}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--octaves", type=int, default=4)
+    ap.add_argument("--scales", type=int, default=5)
+    ap.add_argument("--skip-gauss-planes", action="store_true",
+                    help="keypoints-only mode: do not materialise the Gaussian planes")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            print("bench.py: --gpus %d needs torchrun with %d processes" % (args.gpus, args.gpus), file=sys.stderr)
+            return 2
+
+    import numpy as np
+    import torch
+    import sift_amd
+    from sift_amd.synth import blob_image
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")  # RCCL over xGMI
+    dev = local_rank
+    W, H, O, S = args.width, args.height, args.octaves, args.scales
+    flags = sift_amd.F_SKIP_GAUSS_PLANES if args.skip_gauss_planes else 0
+    params = sift_amd.make_params(O, S, flags=flags)
+
+    img = blob_image(W, H, seed=42 + rank)
+    d_img = torch.from_numpy(img).to("cuda:%d" % dev)
+    torch.cuda.synchronize(dev)
+    ctx = sift_amd.Context(dev)
+
+    kp_rec = sift_amd.KEYPOINT_DTYPE.itemsize
+    gather_state = {"buf": None, "cap": 0}
+
+    def all_gather_keypoints(n):
+        cnt = torch.tensor([n], dtype=torch.int64, device="cuda:%d" % dev)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        m = int(max(int(c.item()) for c in cnts))
+        if gather_state["cap"] < max(m, 1):
+            cap = max(m, 1) + max(m, 1) // 4
+            gather_state["buf"] = torch.empty(cap * kp_rec, dtype=torch.uint8, device="cuda:%d" % dev)
+            gather_state["out"] = torch.empty(world * cap * kp_rec, dtype=torch.uint8, device="cuda:%d" % dev)
+            gather_state["cap"] = cap
+        ctx.copy_keypoints_device(gather_state["buf"].data_ptr(), gather_state["cap"])
+        dist.all_gather_into_tensor(gather_state["out"], gather_state["buf"])
+        return sum(int(c.item()) for c in cnts)
+
+    def step():
+        n = ctx.detect_device(d_img.data_ptr(), W, H, params)
+        if dist is not None:
+            n = all_gather_keypoints(n)
+        return n
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.synchronize()
+    stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0}
+    t0 = time.perf_counter()
+    n_total = 0
+    for _ in range(args.steps):
+        n_total = step()
+        t = ctx.timings()
+        for k in stage:
+            stage[k] += t[k]
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    K = args.steps
+    ms_per_step = elapsed / K * 1e3
+    value = world * W * H / (elapsed / K) / 1e6
+    counts = ctx.counts()
+
+    if rank == 0:
+        gauss_ms = stage["gauss_dog_ms"] / K
+        B = alg_bytes(W, H, O, S, args.skip_gauss_planes)
+        launches = O  # one k_gauss_dog launch per octave
+        achieved = (B / launches) / (gauss_ms / launches * 1e-3) / 1e9
+        cfg_key = "%dx%d_o%d_s%d%s" % (W, H, O, S, "_nogauss" if args.skip_gauss_planes else "")
+        traffic, traffic_src = load_traffic(cfg_key)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": "%dx%d gray f32 image per GPU per step, %d octaves x %d scales, "
+                            "Gaussian+DoG+extrema+refine (keypoints out)%s" %
+                            (W, H, O, S, ", Gaussian planes not materialised" if args.skip_gauss_planes else ""),
+                "width": W, "height": H, "octaves": O, "scales_per_octave": S,
+                "images_per_gpu": 1, "global_batch": world,
+                "parallelism": "dp%d (one image per GPU, RCCL keypoint all-gather)" % world if world > 1 else "single GPU",
+                "planes": "fp32 out, fp64 accumulation/seeds",
+            },
+            "stages_ms": {k: round(v / K, 4) for k, v in stage.items()},
+            "keypoints": counts["keypoints"],
+            "candidates": counts["candidates"],
+            "keypoints_all_ranks": n_total,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_gauss_dog",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "alg_bytes_per_launch": B / launches,
+                "alg_bytes_formula": ("4WH + sum_o 4P_o(S+2) + sum_{o>=1} 8P_o" if args.skip_gauss_planes
+                                      else "4WH + sum_o 4P_o(S+3) + sum_o 4P_o(S+2)"),
+                "launch_ms": round(gauss_ms / launches, 5),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sw, sh = (int(v) for v in args.cpu_sample.split("x"))
+            out["cpu_baseline"] = cpu_baseline(img, O, S, min(sw, W), min(sh, H))
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

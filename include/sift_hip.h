@@ -183,6 +183,11 @@ int sift_last_counts(struct sift_ctx *ctx, size_t *n_candidates, size_t *n_low_c
 
 int sift_last_timings(struct sift_ctx *ctx, sift_timings *t);
 
+/* Device-to-device copy of the last keypoints into caller device memory
+ * (e.g. an RCCL all-gather send buffer), ordered on ctx's stream and
+ * completed before return. */
+int sift_copy_keypoints_device(struct sift_ctx *ctx, void *d_dst, size_t cap, size_t *n_out);
+
 /* Raw device pointers (for in-process consumers that stay on device, e.g.
  * the RCCL all-gather of keypoints).  Valid until the next build/detect. */
 int sift_device_keypoints(struct sift_ctx *ctx, const sift_keypoint **d_kp, size_t *n);

@@ -770,6 +770,19 @@ int sift_last_timings(sift_ctx* ctx, sift_timings* t) {
   return SIFT_OK;
 }
 
+int sift_copy_keypoints_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (n_out) *n_out = ctx->n_kp;
+  if (!d_dst) return SIFT_OK;
+  if (cap < ctx->n_kp) return set_err(ctx, SIFT_E_CAPACITY, "keypoint buffer too small");
+  if (ctx->n_kp) {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(d_dst, ctx->kp.p, ctx->n_kp * sizeof(sift_keypoint), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  return SIFT_OK;
+}
+
 int sift_device_keypoints(sift_ctx* ctx, const sift_keypoint** d_kp, size_t* n) {
   if (!ctx || !d_kp || !n) return SIFT_E_ARG;
   *d_kp = ctx->kp.as<const sift_keypoint>();

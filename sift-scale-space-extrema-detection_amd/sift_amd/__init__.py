@@ -34,7 +34,8 @@ ABI_SYMBOLS = (
     "sift_last_error", "sift_schedule", "sift_octave_dims", "sift_build_scale_space",
     "sift_build_scale_space_device", "sift_get_dims", "sift_get_blur_level", "sift_get_plane",
     "sift_load_dog", "sift_load_scale_space", "sift_find_extrema", "sift_refine",
-    "sift_set_candidates", "sift_copy_candidates", "sift_copy_keypoints", "sift_detect", "sift_detect_device", "sift_last_counts",
+    "sift_set_candidates", "sift_copy_candidates", "sift_copy_keypoints",
+    "sift_copy_keypoints_device", "sift_detect", "sift_detect_device", "sift_last_counts",
     "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
 )
 
@@ -120,6 +121,7 @@ def lib():
         "sift_set_candidates": (ctypes.c_int, [vp, vp, sz]),
         "sift_copy_candidates": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_copy_keypoints": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_copy_keypoints_device": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_detect": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_detect_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
@@ -315,6 +317,13 @@ class Context:
         self._check(self._L.sift_device_keypoints(self._h, ctypes.byref(p), ctypes.byref(n)),
                     "sift_device_keypoints")
         return p.value or 0, n.value
+
+    def copy_keypoints_device(self, d_dst, cap):
+        """D2D copy of the last keypoints into device memory at d_dst (cap records)."""
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_copy_keypoints_device(self._h, ctypes.c_void_p(int(d_dst)), int(cap),
+                                                       ctypes.byref(n)), "sift_copy_keypoints_device")
+        return n.value
 
     def counts(self):
         v = [ctypes.c_size_t() for _ in range(5)]
