@@ -32,6 +32,9 @@ extern "C" {
 
 #define SIFT_ABI_VERSION 1
 
+/* Opaque context (one HIP stream + device-resident pyramids). */
+struct sift_ctx;
+
 /* Status codes.  Every function returns one of these. */
 enum {
   SIFT_OK = 0,
@@ -164,6 +167,11 @@ int sift_refine(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_
  * recomputing (cap in records; SIFT_E_CAPACITY if too small). */
 int sift_copy_candidates(struct sift_ctx *ctx, sift_extremum *out, size_t cap, size_t *n_out);
 int sift_copy_keypoints(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out);
+
+/* Override the two scalars refineCandidateKeypoints receives in its own
+ * message (minBlurLevel, minInterpixelDistance: background.js:460-461,
+ * :611-614) for the next sift_refine; build/load set them from sift_params. */
+int sift_refine_params(struct sift_ctx *ctx, double min_blur_level, double min_interpixel_distance);
 
 /* Use caller-supplied candidates (reference order) for the next sift_refine. */
 int sift_set_candidates(struct sift_ctx *ctx, const sift_extremum *cand, size_t n);

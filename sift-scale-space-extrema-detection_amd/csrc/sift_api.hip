@@ -62,11 +62,13 @@ struct sift_ctx {
   bool have_gauss = false;
   bool have_cand = false;
   size_t n_cand = 0, n_low = 0, n_kp = 0, n_sing = 0, n_exact = 0;
+  size_t n_slots = 0;       // candidate slots (n_cand + entries dropped by the exact pass)
+  bool has_keep = false;    // slots carry keep flags
   // device memory
   DBuf img, seeds, gauss, dog, wts;
-  DBuf ext_keys, ext_pay, srt_keys, srt_pay;   // extrema records
-  DBuf keep, pos, value, flagged;              // candidate ordering
-  DBuf cand_key, cand_val;                     // ordered candidates
+  DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
+  DBuf cand_key, cand_val, cand_keep;          // ordered candidates
+  DBuf keep, pos;                              // keypoint compaction
   DBuf status, kp_tmp, kp, uncertain;          // refinement
   DBuf counters, temp;
   unsigned* h_counters = nullptr;              // pinned mirror of counters
@@ -171,9 +173,9 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   if (!ctx) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->ext_keys,
-                  &ctx->ext_pay, &ctx->srt_keys, &ctx->srt_pay, &ctx->keep, &ctx->pos,
-                  &ctx->value, &ctx->flagged, &ctx->cand_key, &ctx->cand_val, &ctx->status,
+  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
+                  &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
+                  &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->counters, &ctx->temp};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
@@ -464,91 +466,87 @@ static int run_extrema(sift_ctx* ctx) {
   Pyramid& P = ctx->P;
   const bool exact_planes = ctx->dog_source == kForeign;
   unsigned* cnt = ctx->counters.as<unsigned>();
-  const long long tot = total_plane_px(ctx);
-  unsigned cap = (unsigned)std::min<long long>(0x7fffffffLL, std::max<long long>(4096, tot * P.S / 16));
-  if (ctx->ext_keys.bytes >= sizeof(unsigned) * 4096)
-    cap = std::max<unsigned>(cap, (unsigned)std::min<size_t>(0x7fffffff, ctx->ext_keys.bytes / sizeof(unsigned)));
+  // Row / word geometry of the candidate bitmap.
+  std::vector<long long> word_off(P.O), row_off(P.O);
+  long long words = 0, rows = 0;
+  for (int o = 0; o < P.O; ++o) {
+    const int nw = (P.oct[o].w + 63) / 64;
+    word_off[o] = words;
+    row_off[o] = rows;
+    words += (long long)P.S * P.oct[o].h * nw;
+    rows += (long long)P.S * P.oct[o].h;
+  }
+  HIPCHK(ctx->bitmap.ensure((size_t)words * sizeof(unsigned long long)));
+  HIPCHK(ctx->rowcount.ensure((size_t)(rows + 1) * sizeof(unsigned)));
+  HIPCHK(ctx->rowoff.ensure((size_t)(rows + 1) * sizeof(unsigned)));
+  unsigned amb_cap = (unsigned)std::max<size_t>(4096, ctx->amb_keys.bytes / sizeof(unsigned));
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  unsigned n_emit = 0;
+  unsigned n_amb = 0;
   for (int attempt = 0; attempt < 2; ++attempt) {
-    HIPCHK(ctx->ext_keys.ensure((size_t)cap * sizeof(unsigned)));
-    HIPCHK(ctx->ext_pay.ensure((size_t)cap * sizeof(unsigned long long)));
+    HIPCHK(ctx->amb_keys.ensure((size_t)amb_cap * sizeof(unsigned)));
     HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), ctx->stream));
     for (int o = 0; o < P.O; ++o) {
       ExtremaLaunch L{};
       L.o = o;
       L.exact_planes = exact_planes;
-      L.keys = ctx->ext_keys.as<unsigned>();
-      L.payload = ctx->ext_pay.as<unsigned long long>();
+      L.bitmap = ctx->bitmap.as<unsigned long long>() + word_off[o];
+      L.nw = (P.oct[o].w + 63) / 64;
+      L.rowcount = ctx->rowcount.as<unsigned>() + row_off[o];
+      L.amb_keys = ctx->amb_keys.as<unsigned>();
       L.counters = cnt;
-      L.cap = cap;
+      L.amb_cap = amb_cap;
       HIPCHK(launch_extrema(P, L, ctx->stream));
     }
-    HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
+                                            (int)(rows + 1), ctx->stream));
+    HIPCHK(ctx->temp.ensure(tb));
+    tb = ctx->temp.bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
+                                            (int)(rows + 1), ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_counters + 8, ctx->rowoff.as<unsigned>() + rows, sizeof(unsigned),
+                          hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    n_emit = ctx->h_counters[0];
-    if (n_emit <= cap) break;
-    cap = n_emit + n_emit / 8 + 1024;
+    n_amb = ctx->h_counters[0];
+    if (n_amb <= amb_cap) break;
+    amb_cap = n_amb + n_amb / 4 + 1024;
+  }
+  const unsigned n = ctx->h_counters[8];
+  HIPCHK(ctx->cand_key.ensure((size_t)std::max(n, 1u) * sizeof(unsigned)));
+  HIPCHK(ctx->cand_val.ensure((size_t)std::max(n, 1u) * sizeof(double)));
+  HIPCHK(ctx->cand_keep.ensure((size_t)std::max(n, 1u) * sizeof(unsigned)));
+  for (int o = 0; o < P.O; ++o) {
+    EmitLaunch E{};
+    E.o = o;
+    E.bitmap = ctx->bitmap.as<unsigned long long>() + word_off[o];
+    E.nw = (P.oct[o].w + 63) / 64;
+    E.rowcount = ctx->rowcount.as<unsigned>() + row_off[o];
+    E.rowoff = ctx->rowoff.as<unsigned>();
+    E.row_base = (int)row_off[o];
+    E.keys = ctx->cand_key.as<unsigned>();
+    E.value = ctx->cand_val.as<double>();
+    E.keep = ctx->cand_keep.as<unsigned>();
+    HIPCHK(launch_emit(P, E, ctx->stream));
+  }
+  ctx->n_exact = n_amb;
+  if (n_amb) {
+    ExactLaunch X{};
+    X.amb_keys = ctx->amb_keys.as<unsigned>();
+    X.keys = ctx->cand_key.as<unsigned>();
+    X.n = n;
+    X.keep = ctx->cand_keep.as<unsigned>();
+    X.value = ctx->cand_val.as<double>();
+    X.counters = cnt;
+    HIPCHK(launch_exact_extrema(P, X, n_amb, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
   }
   ctx->n_low = ctx->h_counters[1];
-  const int n = (int)n_emit;
-  // Sort records by key (the reference's octave/scale/raster order).
-  unsigned long long maxkey = 0;
-  for (int o = 0; o < P.O; ++o) maxkey = P.oct[o].key_off + (unsigned long long)P.S * P.oct[o].h * P.oct[o].w;
-  int end_bit = 1;
-  while (end_bit < 32 && (1ull << end_bit) <= maxkey) ++end_bit;
-  HIPCHK(ctx->srt_keys.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(ctx->srt_pay.ensure((size_t)std::max(n, 1) * sizeof(unsigned long long)));
-  HIPCHK(ctx->keep.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(ctx->pos.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(ctx->value.ensure((size_t)std::max(n, 1) * sizeof(double)));
-  HIPCHK(ctx->flagged.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(ctx->cand_key.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(ctx->cand_val.ensure((size_t)std::max(n, 1) * sizeof(double)));
-  ctx->n_exact = 0;
-  if (n > 0) {
-    size_t tb = 0, tb2 = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ctx->ext_keys.as<unsigned>(), ctx->srt_keys.as<unsigned>(),
-                                              ctx->ext_pay.as<unsigned long long>(),
-                                              ctx->srt_pay.as<unsigned long long>(), n, 0, end_bit, ctx->stream));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
-                                            ctx->stream));
-    HIPCHK(ctx->temp.ensure(std::max(tb, tb2)));
-    tb = ctx->temp.bytes;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->temp.p, tb, ctx->ext_keys.as<unsigned>(), ctx->srt_keys.as<unsigned>(),
-                                              ctx->ext_pay.as<unsigned long long>(),
-                                              ctx->srt_pay.as<unsigned long long>(), n, 0, end_bit, ctx->stream));
-    CandInit C{};
-    C.keys = ctx->srt_keys.as<unsigned>();
-    C.payload = ctx->srt_pay.as<unsigned long long>();
-    C.n = n;
-    C.keep = ctx->keep.as<unsigned>();
-    C.value = ctx->value.as<double>();
-    C.flagged = ctx->flagged.as<unsigned>();
-    C.counters = cnt;
-    HIPCHK(launch_cand_init(C, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->h_counters + 2, cnt + 2, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    const unsigned nf = ctx->h_counters[2];
-    ctx->n_exact = nf;
-    if (nf) HIPCHK(launch_exact_extrema(P, C, nf, ctx->stream));
-    tb2 = ctx->temp.bytes;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb2, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
-                                            ctx->stream));
-    HIPCHK(launch_scatter_candidates(ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), C.keys, C.value, n,
-                                     ctx->cand_key.as<unsigned>(), ctx->cand_val.as<double>(), ctx->stream));
-    unsigned last[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(&last[0], ctx->pos.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    HIPCHK(hipMemcpyAsync(&last[1], ctx->keep.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->h_counters + 1, cnt + 1, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    ctx->n_cand = (size_t)last[0] + last[1];
-    ctx->n_low = ctx->h_counters[1];
-  } else {
-    ctx->n_cand = 0;
-  }
+  ctx->n_slots = n;
+  ctx->n_cand = n - (n_amb ? ctx->h_counters[2] : 0);
+  ctx->has_keep = true;
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->have_cand = true;
   return SIFT_OK;
@@ -556,7 +554,7 @@ static int run_extrema(sift_ctx* ctx) {
 
 static int run_refine(sift_ctx* ctx) {
   Pyramid& P = ctx->P;
-  const int n = (int)ctx->n_cand;
+  const int n = (int)ctx->n_slots;
   unsigned* cnt = ctx->counters.as<unsigned>();
   HIPCHK(hipEventRecord(ctx->ev[5], ctx->stream));
   HIPCHK(ctx->status.ensure((size_t)std::max(n, 1) * sizeof(int)));
@@ -572,6 +570,7 @@ static int run_refine(sift_ctx* ctx) {
     RefineLaunch R{};
     R.cand_key = ctx->cand_key.as<unsigned>();
     R.cand_val = ctx->cand_val.as<double>();
+    R.keep = ctx->has_keep ? ctx->cand_keep.as<unsigned>() : nullptr;
     R.n = n;
     R.exact_planes = ctx->dog_source == kForeign;
     R.min_blur = ctx->p.min_blur;
@@ -627,17 +626,21 @@ int sift_copy_candidates(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* 
   if (n_out) *n_out = ctx->n_cand;
   if (!out) return SIFT_OK;
   if (cap < ctx->n_cand) return set_err(ctx, SIFT_E_CAPACITY, "candidate buffer too small");
-  const size_t n = ctx->n_cand;
-  std::vector<unsigned> keys(n);
+  const size_t n = ctx->n_slots;
+  std::vector<unsigned> keys(n), keep(n, 1u);
   std::vector<double> vals(n);
   if (n) {
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipMemcpyAsync(keys.data(), ctx->cand_key.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(vals.data(), ctx->cand_val.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->has_keep)
+      HIPCHK(hipMemcpyAsync(keep.data(), ctx->cand_keep.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
   const Pyramid& P = ctx->P;
+  size_t j = 0;
   for (size_t i = 0; i < n; ++i) {
+    if (!keep[i]) continue;
     unsigned k = keys[i];
     int o = 0;
     while (o + 1 < P.O && k >= P.oct[o + 1].key_off) ++o;
@@ -645,12 +648,14 @@ int sift_copy_candidates(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* 
     const unsigned plane = (unsigned)P.oct[o].h * (unsigned)P.oct[o].w;
     const int s = (int)(r / plane) + 1;
     r -= (unsigned)(s - 1) * plane;
-    out[i].octave = o;
-    out[i].scale = s;
-    out[i].y = (int)(r / (unsigned)P.oct[o].w);
-    out[i].x = (int)(r % (unsigned)P.oct[o].w);
-    out[i].value = vals[i];
+    out[j].octave = o;
+    out[j].scale = s;
+    out[j].y = (int)(r / (unsigned)P.oct[o].w);
+    out[j].x = (int)(r % (unsigned)P.oct[o].w);
+    out[j].value = vals[i];
+    ++j;
   }
+  if (n_out) *n_out = j;
   return SIFT_OK;
 }
 
@@ -664,6 +669,14 @@ int sift_find_extrema(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* n_o
   read_stage_times(ctx, true, false);
   if (n_low) *n_low = ctx->n_low;
   return sift_copy_candidates(ctx, out, cap, n_out);
+}
+
+int sift_refine_params(sift_ctx* ctx, double min_blur_level, double min_interpixel_distance) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!(min_blur_level > 0) || !(min_interpixel_distance > 0)) return set_err(ctx, SIFT_E_ARG, "bad refine scalars");
+  ctx->p.min_blur = min_blur_level;
+  ctx->p.min_interpixel_distance = min_interpixel_distance;
+  return SIFT_OK;
 }
 
 int sift_set_candidates(sift_ctx* ctx, const sift_extremum* cand, size_t n) {
@@ -690,6 +703,8 @@ int sift_set_candidates(sift_ctx* ctx, const sift_extremum* cand, size_t n) {
   }
   HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->n_cand = n;
+  ctx->n_slots = n;
+  ctx->has_keep = false;
   ctx->have_cand = true;
   return SIFT_OK;
 }

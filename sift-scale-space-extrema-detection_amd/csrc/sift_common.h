@@ -20,6 +20,9 @@ constexpr int kTX = 64;          // Gaussian tile width  (one wave of columns)
 constexpr int kTY = 32;          // Gaussian tile height (4 waves x 8 rows)
 constexpr int kVT = 8;           // vertical outputs per thread (register sliding window)
 
+// fp64 in the constant address space: uniform indices become scalar loads.
+typedef __attribute__((address_space(4))) const double cdouble;
+
 // Per-octave geometry, passed by value in kernel arguments.
 struct Octave {
   int h, w;

@@ -19,7 +19,7 @@ __device__ inline void wave_L_patch(const Pyramid& P, int o, int t, int y, int x
                                     double* out) {
   const Octave& oc = P.oct[o];
   const int h = oc.h, w = oc.w, r = oc.rad[t];
-  const double* __restrict__ wp = P.wts + oc.wofs[t];
+  const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
   const int lane = threadIdx.x & 63;
   const int nr = 2 * r + 3;
   for (int idx = lane; idx < 3 * nr; idx += 64) {

@@ -1,23 +1,29 @@
-// 26-neighbour extrema scan + ordering (gfx950).
+// 26-neighbour extrema scan with ordered, sort-free emission (gfx950).
 //
 // Replaces findCandidateKeypoints (background.js:359-450) and its kernel
-// SIFT_findExtremas (sift.js:212-316): for DoG scales s = 1..S, a pixel
+// SIFT_findExtremas (sift.js:212-316): for DoG scales s = 1..S a pixel
 // strictly greater (or strictly smaller) than all 26 neighbours, border
-// excluded, is an extremum; |v| >= 0.8*thr makes it a candidate, otherwise it
-// is a low-contrast extremum.
+// excluded, is an extremum; |v| >= 0.8*thr makes it a candidate, otherwise
+// it is a low-contrast extremum.  Output order is the reference's: octave,
+// scale, then raster (y, x).
+//
+// k_extrema: one wave per (scale, band of kXR rows), sweeping 64-column words
+// left to right.  Per word each lane loads its column of the three DoG planes
+// (rows y-1 .. y+kXR), takes x-1 / x+1 from its neighbours with DPP wave
+// shifts (word edges from one extra load), reduces the 26 neighbours with
+// max3/min3, and ballots the candidate mask of the 64 pixels straight into a
+// bitmap word [s][y][x/64].  Row popcounts are exact per wave (no atomics).
+// k_emit expands the bitmap in order after an exclusive scan of the row
+// counts -- the candidate list comes out sorted without a sort.
 //
 // The planes are fp32 roundings of fp64 values.  Rounding is monotone, so an
-// fp32 comparison decides the fp64 one unless the two fp32 values are equal:
-// such ties (and |v| within rounding of 0.8*thr) are flagged and re-decided
-// by k_exact_extrema from an fp64 pointwise recompute.  Records are appended
-// with wave-aggregated atomics, then sorted by key = (octave, scale, y, x),
-// which is exactly the reference's output order (raster order per trio).
+// fp32 comparison decides the fp64 one unless two fp32 values tie; ties and
+// |v| within rounding of 0.8*thr go to a short list that k_exact_extrema
+// re-decides from an fp64 pointwise recompute (sift_exact.h).
 #include "sift_exact.h"
 #include "sift_kernels.h"
 
 namespace sift {
-
-constexpr int kXRows = 16;  // rows per wave in the extrema scan
 
 __device__ __forceinline__ unsigned lane_prefix(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
@@ -34,121 +40,173 @@ __device__ __forceinline__ unsigned wave_append(bool pred, unsigned* counter) {
   return base + lane_prefix(mask);
 }
 
+// Value of lane-1 (lane 0 takes `edge`) / lane+1 (lane 63 takes `edge`).
+__device__ __forceinline__ float from_left(float v, float edge) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float from_right(float v, float edge) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(a, fmaxf(b, c)); }
+__device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(a, fminf(b, c)); }
+
 __global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
   const Octave& oc = P.oct[L.o];
-  const int h = oc.h, w = oc.w;
-  const int s = blockIdx.z + 1;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int x = 1 + blockIdx.x * 64 + lane;
-  const int ybeg = 1 + (blockIdx.y * 4 + wv) * kXRows;
-  if (ybeg > h - 2) return;  // wave-uniform
-  const int yend = min(h - 2, ybeg + kXRows - 1);
+  const int h = oc.h, w = oc.w, S = P.S;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave id
+  const int s = 1 + gw % S;                           // scale fastest: trios of one band run together
+  const int y0 = 1 + (gw / S) * kXR;
+  if (y0 > h - 2) return;                              // wave-uniform
+  const int ny = min(kXR, h - 1 - y0);                 // rows y0 .. y0+ny-1 (<= h-2)
   const long long plane = (long long)h * w;
   const float* __restrict__ D = P.dog + oc.dog_off;
-  const float* __restrict__ Dm = D + (s - 1) * plane;
-  const float* __restrict__ Dc = D + s * plane;
-  const float* __restrict__ Dp = D + (s + 1) * plane;
-  const bool col_ok = x <= w - 2;
-  const int xc = col_ok ? x : 1;  // keep loads in bounds for idle lanes
-
-  // 3 planes x 3 rows x 3 cols sliding down the column.
-  float m[3][3], c[3][3], p[3][3];
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const long long row = (long long)(ybeg - 1 + a) * w + xc - 1;
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      m[a][b] = Dm[row + b];
-      c[a][b] = Dc[row + b];
-      p[a][b] = Dp[row + b];
-    }
-  }
+  const float* Dp[3] = {D + (s - 1) * plane, D + s * plane, D + (s + 1) * plane};
   const double T = P.pix_thr;
-  for (int y = ybeg; y <= yend; ++y) {
-    {
-      const long long row = (long long)(y + 1) * w + xc - 1;
+  unsigned rowcnt[kXR];
 #pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        m[2][b] = Dm[row + b];
-        c[2][b] = Dc[row + b];
-        p[2][b] = Dp[row + b];
-      }
-    }
-    const float v = c[1][1];
-    bool gt = false, lt = false, eq = false;
+  for (int r = 0; r < kXR; ++r) rowcnt[r] = 0;
+  unsigned low = 0;
+  const int edge_dx = lane == 0 ? -1 : 1;
+
+  for (int xw = 0; xw < L.nw; ++xw) {
+    const int x = xw * 64 + lane;
+    const int xc = min(x, w - 1);
+    const int xe = clampi(x + edge_dx, 0, w - 1);
+    // Per plane and row: 3-wide max / min; centre plane also the 2-wide
+    // (x-1, x+1) max / min and the value itself.
+    float hmx[3][kXR + 2], hmn[3][kXR + 2];
+    float emx[kXR + 2], emn[kXR + 2], cv[kXR + 2];
 #pragma unroll
-    for (int a = 0; a < 3; ++a)
+    for (int r = 0; r < kXR + 2; ++r) {
+      const int yy = min(y0 - 1 + r, h - 1);
+      const long long row = (long long)yy * w;
 #pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        gt |= (m[a][b] > v) | (p[a][b] > v);
-        lt |= (m[a][b] < v) | (p[a][b] < v);
-        eq |= (m[a][b] == v) | (p[a][b] == v);
-        if (a != 1 || b != 1) {
-          gt |= c[a][b] > v;
-          lt |= c[a][b] < v;
-          eq |= c[a][b] == v;
+      for (int q = 0; q < 3; ++q) {
+        const float v = Dp[q][row + xc];
+        const float e = Dp[q][row + xe];
+        const float vl = from_left(v, e), vr = from_right(v, e);
+        hmx[q][r] = max3f(vl, v, vr);
+        hmn[q][r] = min3f(vl, v, vr);
+        if (q == 1) {
+          emx[r] = fmaxf(vl, vr);
+          emn[r] = fminf(vl, vr);
+          cv[r] = v;
         }
       }
-    const bool possible = !gt || !lt;         // every neighbour <= v, or every one >= v
-    const bool certain = possible && !eq;     // strict in fp32 => strict in fp64
-    bool ext, tie;
-    if (L.exact_planes) { ext = certain; tie = false; }
-    else { ext = possible; tie = !certain; }
-    ext = ext && col_ok;
-    const double av = fabs((double)v);
-    unsigned flags = tie ? kFlagTie : 0u;
-    bool low_certain;
-    if (L.exact_planes) {
-      low_certain = av < T;
-    } else {
-      const double e = av * 0x1p-24 + 1e-300;  // |v - v_fp64| <= ulp/2 <= |v| 2^-24
-      low_certain = av + e < T;
-      if (!low_certain && av - e < T) flags |= kFlagContrast;
     }
-    const bool count_low = ext && low_certain && !tie;
-    const bool emit = ext && !count_low;
-    const unsigned long long lowmask = __ballot(count_low);
-    if (lowmask && lane == __ffsll((long long)lowmask) - 1) atomicAdd(&L.counters[1], (unsigned)__popcll(lowmask));
-    const unsigned slot = wave_append(emit, &L.counters[0]);
-    if (emit && slot < L.cap) {
-      L.keys[slot] = oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w + (unsigned)x;
-      L.payload[slot] = ((unsigned long long)__float_as_uint(v) << 32) | flags;
-    }
+    const bool col_ok = x >= 1 && x <= w - 2;
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      m[0][b] = m[1][b]; m[1][b] = m[2][b];
-      c[0][b] = c[1][b]; c[1][b] = c[2][b];
-      p[0][b] = p[1][b]; p[1][b] = p[2][b];
+    for (int r = 1; r <= kXR; ++r) {
+      if (r > ny) break;  // wave-uniform
+      const float v = cv[r];
+      const float nmax = max3f(max3f(hmx[0][r - 1], hmx[0][r], hmx[0][r + 1]),
+                               max3f(hmx[2][r - 1], hmx[2][r], hmx[2][r + 1]),
+                               max3f(hmx[1][r - 1], hmx[1][r + 1], emx[r]));
+      const float nmin = min3f(min3f(hmn[0][r - 1], hmn[0][r], hmn[0][r + 1]),
+                               min3f(hmn[2][r - 1], hmn[2][r], hmn[2][r + 1]),
+                               min3f(hmn[1][r - 1], hmn[1][r + 1], emn[r]));
+      const bool possible = v >= nmax || v <= nmin;    // no neighbour strictly beyond v
+      const bool certain = v > nmax || v < nmin;       // strict in fp32 => strict in fp64
+      bool ext, tie;
+      if (L.exact_planes) { ext = certain; tie = false; }
+      else { ext = possible; tie = !certain; }
+      ext = ext && col_ok;
+      const double av = fabs((double)v);
+      bool low_certain, contrast_amb = false;
+      if (L.exact_planes) {
+        low_certain = av < T;
+      } else {
+        const double e = av * 0x1p-24 + 1e-300;  // |v - v_fp64| <= ulp/2 <= |v| 2^-24
+        low_certain = av + e < T;
+        contrast_amb = !low_certain && av - e < T;
+      }
+      const bool count_low = ext && low_certain && !tie;
+      const bool bit = ext && !count_low;
+      low += count_low ? 1u : 0u;
+      const unsigned long long word = __ballot(bit);
+      const int y = y0 + r - 1;
+      if (lane == 0) L.bitmap[((long long)(s - 1) * h + y) * L.nw + xw] = word;
+      rowcnt[r - 1] += (unsigned)__popcll(word);
+      const bool amb = bit && (tie || contrast_amb);
+      const unsigned slot = wave_append(amb, &L.counters[0]);
+      if (amb && slot < L.amb_cap)
+        L.amb_keys[slot] = oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w + (unsigned)x;
     }
   }
-}
-
-__global__ __launch_bounds__(256) void k_cand_init(const CandInit C) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  bool fl = false;
-  if (i < C.n) {
-    const unsigned long long pl = C.payload[i];
-    const unsigned flags = (unsigned)(pl & 0xffffffffull);
-    const float v = __uint_as_float((unsigned)(pl >> 32));
-    C.keep[i] = flags ? 0u : 1u;
-    C.value[i] = (double)v;
-    fl = flags != 0u;
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < kXR; ++r)
+      if (r < ny) L.rowcount[(s - 1) * h + y0 + r] = rowcnt[r];
   }
-  const unsigned slot = wave_append(fl, &C.counters[2]);
-  if (fl) C.flagged[slot] = (unsigned)i;
+  // wave sum of the low-contrast count, one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) low += __shfl_xor(low, off);
+  if (lane == 0 && low) atomicAdd(&L.counters[1], low);
 }
 
-// One 64-thread block (one wave) per flagged candidate.
-__global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const CandInit C) {
+// One wave per (scale, row) of one octave: expand the row's bitmap words in
+// order at the row's offset.  Candidate values are the fp32 plane values
+// (ambiguous ones get their exact fp64 value from k_exact_extrema).
+__global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch E) {
+  const Octave& oc = P.oct[E.o];
+  const int h = oc.h, w = oc.w;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // (s-1)*h + y
+  if (row >= P.S * h) return;
+  const int s = row / h + 1, y = row - (s - 1) * h;
+  if (y < 1 || y > h - 2) return;
+  const unsigned cnt = E.rowcount[row];
+  if (cnt == 0) return;
+  unsigned base = E.rowoff[E.row_base + row];
+  const long long plane = (long long)h * w;
+  const float* __restrict__ Dc = P.dog + oc.dog_off + s * plane + (long long)y * w;
+  const unsigned kbase = oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w;
+  for (int xw0 = 0; xw0 < E.nw; xw0 += 64) {
+    const int xw = xw0 + lane;
+    unsigned long long word = xw < E.nw ? E.bitmap[(long long)row * E.nw + xw] : 0ull;
+    unsigned c = (unsigned)__popcll(word);
+    // inclusive wave scan of c
+    unsigned inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned t = __shfl_up(inc, off);
+      if (lane >= off) inc += t;
+    }
+    unsigned pos = base + inc - c;
+    while (word) {
+      const int b = __ffsll((long long)word) - 1;
+      word &= word - 1;
+      const int x = xw * 64 + b;
+      E.keys[pos] = kbase + (unsigned)x;
+      E.value[pos] = (double)Dc[x];
+      E.keep[pos] = 1u;
+      ++pos;
+    }
+    base += __shfl(inc, 63);
+  }
+}
+
+// One 64-thread block (one wave) per ambiguous candidate: fp64 recompute of
+// the 3x3x3 patch decides extremum and contrast exactly.
+__global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const ExactLaunch X) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const unsigned idx = C.flagged[blockIdx.x];
+  const unsigned key = X.amb_keys[blockIdx.x];
+  // position of key in the ordered candidate list (binary search)
+  unsigned lo = 0, hi = X.n;
+  while (lo < hi) {
+    const unsigned mid = (lo + hi) >> 1;
+    if (X.keys[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  const unsigned idx = lo;
   int o, s, y, x;
-  decode_key(P, C.keys[idx], o, s, y, x);
+  decode_key(P, key, o, s, y, x);
   double* d27 = smem;
   double* Lbuf = smem + 32;
   double* sh = smem + 32 + 40;
   wave_dog_patch(P, o, s, y, x, sh, Lbuf, d27);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && idx < X.n && X.keys[idx] == key) {
     const double v = d27[13];
     bool gt = false, lt = false;
     for (int q = 0; q < 27; ++q) {
@@ -158,37 +216,27 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Can
     }
     const bool ext = !gt || !lt;
     const bool cand = ext && fabs(v) >= P.pix_thr;
-    C.keep[idx] = cand ? 1u : 0u;
-    C.value[idx] = v;
-    if (ext && !cand) atomicAdd(&C.counters[1], 1u);
-  }
-}
-
-__global__ __launch_bounds__(256) void k_scatter_cand(const unsigned* __restrict__ keep,
-                                                      const unsigned* __restrict__ pos,
-                                                      const unsigned* __restrict__ keys,
-                                                      const double* __restrict__ val, int n,
-                                                      unsigned* __restrict__ out_key,
-                                                      double* __restrict__ out_val) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n && keep[i]) {
-    out_key[pos[i]] = keys[i];
-    out_val[pos[i]] = val[i];
+    X.keep[idx] = cand ? 1u : 0u;
+    X.value[idx] = v;
+    if (ext && !cand) atomicAdd(&X.counters[1], 1u);
+    if (!cand) atomicAdd(&X.counters[2], 1u);  // dropped entries
   }
 }
 
 hipError_t launch_extrema(const Pyramid& P, const ExtremaLaunch& L, hipStream_t st) {
   const Octave& oc = P.oct[L.o];
   if (oc.h < 3 || oc.w < 3 || P.S < 1) return hipSuccess;  // no interior pixels
-  const int inner_h = oc.h - 2, inner_w = oc.w - 2;
-  dim3 grid((inner_w + 63) / 64, (inner_h + 4 * kXRows - 1) / (4 * kXRows), P.S);
-  hipLaunchKernelGGL(k_extrema, grid, dim3(256), 0, st, P, L);
+  const int bands = (oc.h - 2 + kXR - 1) / kXR;
+  const int waves = bands * P.S;
+  hipLaunchKernelGGL(k_extrema, dim3((waves + 3) / 4), dim3(256), 0, st, P, L);
   return hipGetLastError();
 }
 
-hipError_t launch_cand_init(const CandInit& C, hipStream_t st) {
-  if (C.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_cand_init, dim3((C.n + 255) / 256), dim3(256), 0, st, C);
+hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st) {
+  const Octave& oc = P.oct[E.o];
+  if (oc.h < 3 || oc.w < 3) return hipSuccess;
+  const int rows = P.S * oc.h;
+  hipLaunchKernelGGL(k_emit, dim3((rows + 3) / 4), dim3(256), 0, st, P, E);
   return hipGetLastError();
 }
 
@@ -198,19 +246,9 @@ size_t exact_lds_bytes(const Pyramid& P) {
   return sizeof(double) * (size_t)(32 + 40 + exact_scratch_doubles(rmax));
 }
 
-hipError_t launch_exact_extrema(const Pyramid& P, const CandInit& C, unsigned n_flagged,
-                                hipStream_t st) {
-  if (n_flagged == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_exact_extrema, dim3(n_flagged), dim3(64), exact_lds_bytes(P), st, P, C);
-  return hipGetLastError();
-}
-
-hipError_t launch_scatter_candidates(const unsigned* keep, const unsigned* pos, const unsigned* keys,
-                                     const double* val, int n, unsigned* out_key, double* out_val,
-                                     hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter_cand, dim3((n + 255) / 256), dim3(256), 0, st, keep, pos, keys, val, n,
-                     out_key, out_val);
+hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, unsigned n_amb, hipStream_t st) {
+  if (n_amb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_exact_extrema, dim3(n_amb), dim3(64), exact_lds_bytes(P), st, P, X);
   return hipGetLastError();
 }
 

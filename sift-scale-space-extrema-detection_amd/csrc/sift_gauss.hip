@@ -22,29 +22,33 @@
 
 namespace sift {
 
-template <bool BASE_LDS>
+template <bool BASE_LDS, bool OCT0>
 __global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const Octave& oc = P.oct[L.o];
   const int h = oc.h, w = oc.w, R = oc.rmax;
   const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
-  const int tid = threadIdx.x, lane = tid & 63, ty = (tid >> 6) * kVT;
-  const double* __restrict__ wts = P.wts;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ty = wv * kVT;
 
   // Rows this tile can touch, clamped: the strip only holds distinct rows.
   const int lo_all = max(0, y0 - R), hi_all = min(h - 1, y0 + kTY - 1 + R);
   const int BW = kTX + 2 * R;
   double* sH = smem;
   double* sB = smem + (size_t)(hi_all - lo_all + 1) * kTX;
+  const float* __restrict__ img = P.img;
+  const double* __restrict__ seed = P.seeds + oc.seed_off;
+  auto base = [&](int y, int x) -> double {  // y, x already clamped
+    if (OCT0) return (double)img[(long long)(y >> 1) * P.img_stride + (x >> 1)];
+    return seed[(long long)y * w + x];
+  };
 
   if (BASE_LDS) {
-    // Replicated-edge base region: rows y0-R .. y0+kTY+R-1 restricted to the
-    // clamped range, columns x0-R .. x0+kTX+R-1 with clamped sources.
+    // Replicated-edge base region: rows lo_all..hi_all, columns x0-R ..
+    // x0+kTX+R-1 with clamped sources.
     const int nr = hi_all - lo_all + 1;
     for (int idx = tid; idx < nr * BW; idx += 256) {
       const int rr = idx / BW, cc = idx - rr * BW;
-      const int x = clampi(x0 - R + cc, 0, w - 1);
-      sB[idx] = base_at(P, L.o, lo_all + rr, x);
+      sB[idx] = base(lo_all + rr, clampi(x0 - R + cc, 0, w - 1));
     }
     __syncthreads();
   }
@@ -57,23 +61,45 @@ __global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussL
 
   for (int s = 0; s < P.NS; ++s) {
     const int r = oc.rad[s];
-    const double* __restrict__ wp = wts + oc.wofs[s];
+    // Taps through the constant address space: wave-uniform scalar loads.
+    const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
     const int lo = max(0, y0 - r), hi = min(h - 1, y0 + kTY - 1 + r);
     const int nrows = hi - lo + 1;
 
-    // Horizontal pass: sH[y - lo][c] = sum_i w_i * B(y, clamp(x0 + c - r + i)).
-    for (int idx = tid; idx < nrows * kTX; idx += 256) {
-      const int rr = idx >> 6, c = idx & 63;
-      const int y = lo + rr;
-      double acc = 0.0;
+    // Horizontal pass: sH[y - lo][c] = sum_i w_i * B(y, clamp(x0 + c - r + i)),
+    // four independent rows per thread (wave rows wv*4 .. +3 of each group of 16).
+    for (int rb = wv * 4; rb < nrows; rb += 16) {
+      const int r0 = rb, r1 = min(rb + 1, nrows - 1), r2 = min(rb + 2, nrows - 1), r3 = min(rb + 3, nrows - 1);
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       if (BASE_LDS) {
-        const double* row = sB + (size_t)(y - lo_all) * BW + (c + R - r);
-        for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], row[i], acc);
+        const int cb = lane + R - r;
+        const double* p0 = sB + (size_t)(lo + r0 - lo_all) * BW + cb;
+        const double* p1 = sB + (size_t)(lo + r1 - lo_all) * BW + cb;
+        const double* p2 = sB + (size_t)(lo + r2 - lo_all) * BW + cb;
+        const double* p3 = sB + (size_t)(lo + r3 - lo_all) * BW + cb;
+#pragma unroll 2
+        for (int i = 0; i <= 2 * r; ++i) {
+          const double wi = wp[i];
+          a0 = fma(wi, p0[i], a0);
+          a1 = fma(wi, p1[i], a1);
+          a2 = fma(wi, p2[i], a2);
+          a3 = fma(wi, p3[i], a3);
+        }
       } else {
-        const int xb = x0 + c - r;
-        for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], base_at(P, L.o, y, clampi(xb + i, 0, w - 1)), acc);
+        const int xb = x0 + lane - r;
+        for (int i = 0; i <= 2 * r; ++i) {
+          const double wi = wp[i];
+          const int xx = clampi(xb + i, 0, w - 1);
+          a0 = fma(wi, base(lo + r0, xx), a0);
+          a1 = fma(wi, base(lo + r1, xx), a1);
+          a2 = fma(wi, base(lo + r2, xx), a2);
+          a3 = fma(wi, base(lo + r3, xx), a3);
+        }
       }
-      sH[idx] = acc;
+      sH[r0 * kTX + lane] = a0;
+      if (rb + 1 < nrows) sH[r1 * kTX + lane] = a1;
+      if (rb + 2 < nrows) sH[r2 * kTX + lane] = a2;
+      if (rb + 3 < nrows) sH[r3 * kTX + lane] = a3;
     }
     __syncthreads();
 
@@ -128,23 +154,28 @@ size_t gauss_lds_bytes(const Octave& oc, bool base_lds) {
   return b;
 }
 
+template <bool BL, bool O0>
+static void set_lds_attr() {
+  (void)hipFuncSetAttribute((const void*)k_gauss_dog<BL, O0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t st) {
   const Octave& oc = P.oct[L.o];
   dim3 grid((oc.w + kTX - 1) / kTX, (oc.h + kTY - 1) / kTY);
   const size_t lds = gauss_lds_bytes(oc, L.base_lds);
   static bool attr_set = false;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute((const void*)k_gauss_dog<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_gauss_dog<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    set_lds_attr<true, true>();
+    set_lds_attr<true, false>();
+    set_lds_attr<false, true>();
+    set_lds_attr<false, false>();
     attr_set = true;
   }
-  if (L.base_lds) {
-    hipLaunchKernelGGL(k_gauss_dog<true>, grid, dim3(256), lds, st, P, L);
-  } else {
-    hipLaunchKernelGGL(k_gauss_dog<false>, grid, dim3(256), lds, st, P, L);
-  }
+  const bool o0 = L.o == 0;
+  if (L.base_lds && o0) hipLaunchKernelGGL((k_gauss_dog<true, true>), grid, dim3(256), lds, st, P, L);
+  else if (L.base_lds) hipLaunchKernelGGL((k_gauss_dog<true, false>), grid, dim3(256), lds, st, P, L);
+  else if (o0) hipLaunchKernelGGL((k_gauss_dog<false, true>), grid, dim3(256), lds, st, P, L);
+  else hipLaunchKernelGGL((k_gauss_dog<false, false>), grid, dim3(256), lds, st, P, L);
   return hipGetLastError();
 }
 

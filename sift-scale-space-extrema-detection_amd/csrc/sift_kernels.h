@@ -21,28 +21,44 @@ struct GaussLaunch {
   int base_lds;       // stage the replicated-edge base region in LDS
 };
 
+constexpr int kXR = 8;  // rows per wave in the extrema scan
+
 struct ExtremaLaunch {
   int o;
-  int exact_planes;            // DoG planes are the data itself (caller-supplied): no fp32 ties
-  unsigned* keys;              // candidate sort keys (unordered)
-  unsigned long long* payload; // float bits << 32 | flags
-  unsigned* counters;          // [0] emitted, [1] certain low-contrast
-  unsigned cap;
+  int exact_planes;              // DoG planes are the data itself (caller-supplied): no fp32 ties
+  unsigned long long* bitmap;    // this octave's candidate bitmap [S][h][nw]
+  int nw;                        // 64-pixel words per row
+  unsigned* rowcount;            // this octave's candidates per (scale, row) [S][h]
+  unsigned* amb_keys;            // keys needing an exact fp64 decision (unordered)
+  unsigned* counters;            // [0] ambiguous, [1] low-contrast, [2] dropped by exact pass
+  unsigned amb_cap;
 };
 
-struct CandInit {
-  const unsigned* keys;              // sorted
-  const unsigned long long* payload; // sorted alongside
-  int n;
-  unsigned* keep;     // out: 1 = candidate
-  double* value;      // out: DoG value (exact fp64 where re-decided)
-  unsigned* flagged;  // out: indices needing an exact decision
-  unsigned* counters; // [2] n flagged, [1] low-contrast (exact decisions add here)
+struct EmitLaunch {
+  int o;
+  const unsigned long long* bitmap;
+  int nw;
+  const unsigned* rowcount;      // this octave's [S][h]
+  const unsigned* rowoff;        // exclusive scan over all octaves' row counts
+  int row_base;                  // index of this octave's first row in rowoff
+  unsigned* keys;                // ordered candidate keys
+  double* value;
+  unsigned* keep;
+};
+
+struct ExactLaunch {
+  const unsigned* amb_keys;
+  const unsigned* keys;          // ordered candidates
+  unsigned n;
+  unsigned* keep;
+  double* value;
+  unsigned* counters;
 };
 
 struct RefineLaunch {
   const unsigned* cand_key;
   const double* cand_val;
+  const unsigned* keep;  // nullptr = every entry is a candidate
   int n;
   int exact_planes;
   double min_blur, min_interpixel_distance;
@@ -57,24 +73,19 @@ hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t 
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
 
 hipError_t launch_extrema(const Pyramid& P, const ExtremaLaunch& L, hipStream_t st);
-hipError_t launch_cand_init(const CandInit& C, hipStream_t st);
-// One wave per flagged candidate: fp64 pointwise recompute of the 3x3x3 DoG patch.
-hipError_t launch_exact_extrema(const Pyramid& P, const CandInit& C, unsigned n_flagged,
-                                hipStream_t st);
+hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st);
+// One wave per ambiguous candidate: fp64 pointwise recompute of the 3x3x3 DoG patch.
+hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, unsigned n_amb, hipStream_t st);
 
 hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream_t st);
 hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, unsigned n_uncertain,
                                hipStream_t st);
 
 // Order-preserving compaction helpers.
-hipError_t launch_scatter_candidates(const unsigned* keep, const unsigned* pos, const unsigned* keys,
-                                     const double* val, int n, unsigned* out_key, double* out_val,
-                                     hipStream_t st);
 hipError_t launch_scatter_keypoints(const int* status, const unsigned* pos, const Keypoint* kp,
                                     int n, Keypoint* out, hipStream_t st);
 hipError_t launch_status_to_keep(const int* status, unsigned* keep, int n, hipStream_t st);
 
-// Exact fp64 DoG patch for host-side checks (tests): d[27] for (o, s, y, x).
 size_t exact_lds_bytes(const Pyramid& P);
 
 }  // namespace sift

@@ -176,7 +176,9 @@ __device__ inline void make_keypoint(Keypoint& k, int o, const StepOut& R, int S
 __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const RefineLaunch L) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool unc = false;
-  if (i < L.n) {
+  if (i < L.n && L.keep && !L.keep[i]) {
+    L.status[i] = kRefDiscard;
+  } else if (i < L.n) {
     int o, s, m, n;
     decode_key(P, L.cand_key[i], o, s, m, n);
     const Octave& oc = P.oct[o];

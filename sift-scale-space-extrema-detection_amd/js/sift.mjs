@@ -1,0 +1,410 @@
+// sift.mjs -- the reference's call surface, backed by the MI355X HIP path.
+//
+// Drop-in for the hot path of bingjetli/sift-scale-space-extrema-detection:
+//   computeGaussianScaleSpace   background.js:71   (worker.js:29 argument names/defaults)
+//   computeDifferenceOfGaussians background.js:258 (worker.js:54)
+//   findCandidateKeypoints      background.js:359  (worker.js:64)
+//   refineCandidateKeypoints    background.js:455  (worker.js:81)
+//   WorkerMessageTypes          src/worker.js:5-24
+//   createWorkerHandler         background.js:14-50 (message dispatcher)
+// plus the north-star aliases buildScaleSpace / findCandidateKeypoints and a
+// one-call detect()/detectAsync().
+//
+// Images are ImageData-shaped gray Float32: {width, height, data: Float32Array}.
+// A Matrix2D (nested arrays, matrix2d.js) is accepted and rounded to fp32.
+// Planes come back ImageData-shaped, or as Matrix2D with {matrix2d: true}
+// (what main.js-style callers index as image[y][x]).
+//
+// Results of one stage carry a hidden handle to the device-resident state, so
+// chaining the stages on their own outputs never re-uploads a pyramid; any
+// other input (edited or foreign arrays) is uploaded and processed as given.
+import { createRequire } from 'module';
+
+const require = createRequire(import.meta.url);
+const native = require('../napi/sift_napi.node');
+
+export const WorkerMessageTypes = {
+  COMPUTE_GAUSSIAN_SCALE_SPACE: 'compute-gaussian-scale-space',
+  RECEIVED_GAUSSIAN_SCALE_SPACE: 'received-gaussian-scale-space',
+  RECEIVED_GAUSSIAN_BLURRED_CHUNK: 'received-gaussian-blurred-chunk',
+  RECEIVED_GAUSSIAN_BLURRED_IMAGE: 'received-gaussian-blurred-image',
+
+  COMPUTE_DIFFERENCE_OF_GAUSSIANS: 'compute-difference-of-gaussians',
+  RECEIVED_DIFFERENCE_OF_GAUSSIANS: 'received-difference-of-gaussians',
+  RECEIVED_DIFFERENCE_OF_GAUSSIAN_CHUNK: 'received-difference-of-gaussian-chunk',
+  RECEIVED_DIFFERENCE_OF_GAUSSIAN_IMAGE: 'received-difference-of-gaussian-image',
+
+  FIND_CANDIDATE_KEYPOINTS: 'find-candidate-keypoints',
+  RECEIVED_CANDIDATE_KEYPOINT_IMAGE: 'received-candidate-keypoint-image',
+  RECEIVED_CANDIDATE_KEYPOINT_BASE_IMAGE: 'received-candidate-keypoint-base-image',
+  RECEIVED_CANDIDATE_KEYPOINT_MARKER: 'received-candidate-keypoint-marker',
+  RECEIVED_CANDIDATE_KEYPOINTS: 'received-candidate-keypoints',
+
+  REFINE_CANDIDATE_KEYPOINTS: 'refine-candidate-keypoints',
+  RECEIVED_REFINED_KEYPOINTS: 'received-refined-keypoints',
+};
+
+const PLANE_GAUSS = 0;
+const PLANE_DOG = 1;
+const HANDLE = Symbol('sift-device-state');
+
+// ---------------------------------------------------------------------------
+// Device contexts (one per device, created lazily).
+// ---------------------------------------------------------------------------
+const contexts = new Map();
+
+function deviceState(device = 0) {
+  let st = contexts.get(device);
+  if (!st) {
+    st = { ctx: native.createContext(device), gen: 0, stage: null, W: 0, H: 0, params: null };
+    contexts.set(device, st);
+  }
+  return st;
+}
+
+function bump(st, stage, W, H, params) {
+  st.gen += 1;
+  st.stage = stage;
+  st.W = W;
+  st.H = H;
+  st.params = params;
+  return st.gen;
+}
+
+function attach(obj, st, gen, extra) {
+  Object.defineProperty(obj, HANDLE, { value: Object.assign({ st, gen }, extra), enumerable: false });
+  return obj;
+}
+
+function liveHandle(obj) {
+  const h = obj && obj[HANDLE];
+  return h && h.st.gen === h.gen ? h : null;
+}
+
+// ---------------------------------------------------------------------------
+// Images.
+// ---------------------------------------------------------------------------
+function isMatrix2D(m) {
+  return Array.isArray(m) && m.length > 0 && (Array.isArray(m[0]) || ArrayBuffer.isView(m[0]));
+}
+
+function toGray(img) {
+  if (img && ArrayBuffer.isView(img.data) && img.width > 0 && img.height > 0) {
+    const n = img.width * img.height;
+    if (img.data.length < n) throw new TypeError('image.data is shorter than width*height');
+    const data = img.data instanceof Float32Array ? img.data : Float32Array.from(img.data.subarray(0, n));
+    return { width: img.width, height: img.height, data };
+  }
+  if (isMatrix2D(img)) {
+    const height = img.length, width = img[0].length;
+    const data = new Float32Array(width * height);
+    for (let y = 0; y < height; y++) {
+      const row = img[y];
+      for (let x = 0; x < width; x++) data[y * width + x] = row[x];
+    }
+    return { width, height, data };
+  }
+  throw new TypeError('expected an ImageData-shaped {width, height, data} gray image or a Matrix2D');
+}
+
+function planeImage(data, width, height, matrix2d) {
+  if (!matrix2d) return { width, height, data };
+  const out = new Array(height);
+  for (let y = 0; y < height; y++) out[y] = Array.from(data.subarray(y * width, (y + 1) * width));
+  return out;
+}
+
+function planeDims(image) {
+  if (isMatrix2D(image)) return [image.length, image[0].length];
+  return [image.height, image.width];
+}
+
+function planeData(image) {
+  if (isMatrix2D(image)) return toGray(image).data;
+  return image.data instanceof Float32Array ? image.data : Float32Array.from(image.data);
+}
+
+function flatten(pyramid) {
+  let total = 0;
+  for (const oct of pyramid) for (const e of oct) { const [h, w] = planeDims(e.image); total += h * w; }
+  const flat = new Float32Array(total);
+  let off = 0;
+  for (const oct of pyramid) for (const e of oct) { const d = planeData(e.image); flat.set(d, off); off += d.length; }
+  return flat;
+}
+
+// Input (W, H) of a pyramid: octave 0 is the 2x upsample (background.js:84).
+function inputDimsOf(pyramid) {
+  const [h0, w0] = planeDims(pyramid[0][0].image);
+  return [w0 / 2, h0 / 2];
+}
+
+// ---------------------------------------------------------------------------
+// Schedule in JS, exactly as background.js:89-177 computes it (Math.pow),
+// handed to the native side so blur levels and sigmas are bit-identical.
+// ---------------------------------------------------------------------------
+export function scaleSchedule(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur) {
+  const NS = scales_per_octave + 3;
+  const blur = new Float64Array(number_of_octaves * NS);
+  const sigma = new Float64Array(number_of_octaves * NS);
+  const k = Math.pow(2, 1 / scales_per_octave);
+  let base = min_blur_level;
+  for (let o = 0; o < number_of_octaves; o++) {
+    for (let s = 0; s < NS; s++) {
+      if (o > 0 && s === 0) {
+        base = blur[(o - 1) * NS + scales_per_octave];
+        blur[o * NS] = base;
+        sigma[o * NS] = 0;
+      } else {
+        const target = base * Math.pow(k, s);
+        const from = o === 0 ? assumed_blur : base;
+        blur[o * NS + s] = target;
+        sigma[o * NS + s] = Math.sqrt((target * target) - (from * from));
+      }
+    }
+  }
+  return { blur, sigma };
+}
+
+function nativeParams(O, S, min_blur, assumed_blur, mid = 0.5) {
+  return { num_octaves: O, scales_per_octave: S, min_blur, assumed_blur, min_interpixel_distance: mid };
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1: computeGaussianScaleSpace (background.js:71-237).  The DoG of
+// background.js:258 is formed in the same device pass and kept resident.
+// ---------------------------------------------------------------------------
+export function computeGaussianScaleSpace(args, ...rest) {
+  let a = args;
+  if (!a || a.input_image === undefined) {
+    // positional form of background.js:71
+    a = { input_image: args, number_of_octaves: rest[0], scales_per_octave: rest[1],
+      min_blur_level: rest[2], assumed_blur: rest[3], chunk_size: rest[4], ...(rest[5] || {}) };
+  }
+  const {
+    input_image, number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8,
+    assumed_blur = 0.5, device = 0, matrix2d = false,
+  } = a;  // chunk_size only shaped the reference's progress messages; it never changes values
+  const img = toGray(input_image);
+  const st = deviceState(device);
+  const { blur, sigma } = scaleSchedule(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur);
+  const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur);
+  native.buildScaleSpace(st.ctx, img.data, img.width, img.height, params, sigma);
+  const gen = bump(st, 'built', img.width, img.height, params);
+  const NS = scales_per_octave + 3;
+  const scaleSpace = [];
+  for (let o = 0; o < number_of_octaves; o++) {
+    const [h, w] = native.getDims(st.ctx, o);
+    const oct = [];
+    for (let s = 0; s < NS; s++) {
+      oct.push({ blurLevel: blur[o * NS + s], image: planeImage(native.getPlane(st.ctx, PLANE_GAUSS, o, s), w, h, matrix2d) });
+    }
+    scaleSpace.push(oct);
+  }
+  return attach(scaleSpace, st, gen, { blur, matrix2d, params });
+}
+export const buildScaleSpace = computeGaussianScaleSpace;
+
+// ---------------------------------------------------------------------------
+// Stage 2: computeDifferenceOfGaussians (background.js:258-354):
+// D[s-1] = L[s-1] - L[s], blurLevel of L[s-1].
+// ---------------------------------------------------------------------------
+export function computeDifferenceOfGaussians(scale_space, chunk_size = 32, { device = 0, matrix2d } = {}) {
+  void chunk_size;
+  let h = liveHandle(scale_space);
+  let st, gen, blur, asM;
+  if (h) {
+    ({ st, gen } = h);
+    blur = h.blur;
+    asM = matrix2d === undefined ? h.matrix2d : matrix2d;
+  } else {
+    st = deviceState(device);
+    const O = scale_space.length, NS = scale_space[0].length;
+    const [W, H] = inputDimsOf(scale_space);
+    const params = nativeParams(O, NS - 3, 0.8, 0.5);
+    native.loadScaleSpace(st.ctx, flatten(scale_space), W, H, params);
+    gen = bump(st, 'foreign-gauss', W, H, params);
+    blur = new Float64Array(O * NS);
+    for (let o = 0; o < O; o++) for (let s = 0; s < NS; s++) blur[o * NS + s] = scale_space[o][s].blurLevel;
+    asM = matrix2d === undefined ? isMatrix2D(scale_space[0][0].image) : matrix2d;
+  }
+  const O = scale_space.length, NS = scale_space[0].length;
+  const dog = [];
+  for (let o = 0; o < O; o++) {
+    const [hh, ww] = native.getDims(st.ctx, o);
+    const oct = [];
+    for (let s = 1; s < NS; s++) {
+      oct.push({ blurLevel: blur[o * NS + s - 1], image: planeImage(native.getPlane(st.ctx, PLANE_DOG, o, s - 1), ww, hh, asM) });
+    }
+    dog.push(oct);
+  }
+  return attach(dog, st, gen, {});
+}
+
+function ensureDog(differenceOfGaussians, scalesPerOctave, device) {
+  const h = liveHandle(differenceOfGaussians);
+  if (h) return h.st;
+  const st = deviceState(device);
+  const O = differenceOfGaussians.length;
+  const S = differenceOfGaussians[0].length - 2;
+  if (scalesPerOctave !== undefined && scalesPerOctave !== S) {
+    // the reference would index past the pyramid; keep its threshold argument but the data's shape
+  }
+  const [W, H] = inputDimsOf(differenceOfGaussians);
+  const params = nativeParams(O, S, 0.8, 0.5);
+  native.loadDog(st.ctx, flatten(differenceOfGaussians), W, H, params);
+  const gen = bump(st, 'foreign-dog', W, H, params);
+  attach(differenceOfGaussians, st, gen, {});
+  return st;
+}
+
+// ---------------------------------------------------------------------------
+// Stage 3: findCandidateKeypoints (background.js:359-450).
+// Output [octave][scale-1] = {scaleLevel, localExtremas: [{x, y, value}]}.
+// ---------------------------------------------------------------------------
+export function findCandidateKeypoints(args, octave_base_images, scales_per_octave) {
+  let a = args;
+  if (!a || a.differenceOfGaussians === undefined) {
+    a = { differenceOfGaussians: args, octaveBaseImages: octave_base_images, scalesPerOctave: scales_per_octave };
+  }
+  const { differenceOfGaussians, scalesPerOctave, device = 0 } = a;  // octaveBaseImages: unused (background.js:361)
+  const st = ensureDog(differenceOfGaussians, scalesPerOctave, device);
+  const r = native.findExtrema(st.ctx);
+  const O = differenceOfGaussians.length;
+  const S = differenceOfGaussians[0].length - 2;
+  const out = [];
+  for (let o = 0; o < O; o++) {
+    const oct = [];
+    for (let s = 1; s <= S; s++) oct.push({ scaleLevel: s, localExtremas: [] });
+    out.push(oct);
+  }
+  const n = r.values.length;
+  for (let i = 0; i < n; i++) {
+    const o = r.ints[4 * i], s = r.ints[4 * i + 1];
+    out[o][s - 1].localExtremas.push({ x: r.ints[4 * i + 2], y: r.ints[4 * i + 3], value: r.values[i] });
+  }
+  Object.defineProperty(out, 'lowContrastCount', { value: r.lowContrast, enumerable: false });
+  return attach(out, st, st.gen, { n });
+}
+
+// ---------------------------------------------------------------------------
+// Stage 4: refineCandidateKeypoints (background.js:455-685).  Like the
+// reference, a Hessian with |det| < Number.EPSILON raises a TypeError and no
+// list is returned (matrix2d.js:482 -> :455).
+// ---------------------------------------------------------------------------
+export function refineCandidateKeypoints(args, candidate_keypoints, scales_per_octave, number_of_octaves,
+  min_blur_level, min_interpixel_distance = 0.5) {
+  let a = args;
+  if (!a || a.differenceOfGaussians === undefined) {
+    a = { differenceOfGaussians: args, candidateKeypoints: candidate_keypoints, scalesPerOctave: scales_per_octave,
+      numberOfOctaves: number_of_octaves, minBlurLevel: min_blur_level, minInterpixelDistance: min_interpixel_distance };
+  }
+  const {
+    differenceOfGaussians, scalesPerOctave, numberOfOctaves, candidateKeypoints, minBlurLevel,
+    minInterpixelDistance = 0.5, device = 0, throwOnSingular = true,
+  } = a;
+  const st = ensureDog(differenceOfGaussians, scalesPerOctave, device);
+  const hc = liveHandle(candidateKeypoints);
+  if (!hc) {
+    // upload the (possibly edited or foreign) candidate lists in reference order (background.js:468-471)
+    let n = 0;
+    for (let o = 0; o < numberOfOctaves; o++) for (let s = 0; s < scalesPerOctave; s++) n += candidateKeypoints[o][s].localExtremas.length;
+    const ints = new Int32Array(4 * n), vals = new Float64Array(n);
+    let i = 0;
+    for (let o = 0; o < numberOfOctaves; o++) {
+      for (let s = 0; s < scalesPerOctave; s++) {
+        const sc = candidateKeypoints[o][s];
+        for (const e of sc.localExtremas) {
+          ints[4 * i] = o; ints[4 * i + 1] = sc.scaleLevel; ints[4 * i + 2] = e.x; ints[4 * i + 3] = e.y;
+          vals[i] = e.value;
+          i++;
+        }
+      }
+    }
+    native.setCandidates(st.ctx, ints, vals);
+  }
+  native.setRefineParams(st.ctx, minBlurLevel === undefined ? 0.8 : minBlurLevel, minInterpixelDistance);
+  const r = native.refine(st.ctx);
+  if (r.singular > 0 && throwOnSingular) {
+    throw new TypeError("Cannot read property 'length' of null (singular Hessian in refinement, as in the reference)");
+  }
+  return keypointsFromNative(r);
+}
+
+function keypointsFromNative(r) {
+  const n = r.ints.length / 4;
+  const out = new Array(n);
+  for (let i = 0; i < n; i++) {
+    out[i] = {
+      octave: r.ints[4 * i], scaleLevel: r.ints[4 * i + 1], localX: r.ints[4 * i + 2], localY: r.ints[4 * i + 3],
+      absoluteSigma: r.doubles[4 * i], absoluteX: r.doubles[4 * i + 1], absoluteY: r.doubles[4 * i + 2],
+      interpolatedValue: r.doubles[4 * i + 3],
+    };
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// One-call fast path: all four stages on device, keypoints out.
+// ---------------------------------------------------------------------------
+export function detect(input_image, { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8,
+  assumed_blur = 0.5, min_interpixel_distance = 0.5, device = 0 } = {}) {
+  const img = toGray(input_image);
+  const st = deviceState(device);
+  const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
+  const r = native.detect(st.ctx, img.data, img.width, img.height, params);
+  bump(st, 'detected', img.width, img.height, params);
+  return keypointsFromNative(r);
+}
+
+export async function detectAsync(input_image, opts = {}) {
+  const { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8, assumed_blur = 0.5,
+    min_interpixel_distance = 0.5, device = 0 } = opts;
+  const img = toGray(input_image);
+  const st = deviceState(device);
+  const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
+  bump(st, 'detecting', img.width, img.height, params);
+  const r = await native.detectAsync(st.ctx, img.data, img.width, img.height, params);
+  return keypointsFromNative(r);
+}
+
+export function lastCounts(device = 0) {
+  return native.counts(deviceState(device).ctx);
+}
+
+// ---------------------------------------------------------------------------
+// background.js-compatible dispatcher (background.js:14-50): returns an
+// onmessage(e) that answers each request with the reference's RECEIVED_*
+// message.  Pyramids go out as Matrix2D by default, as the reference posts
+// them (main.js indexes image[y][x]).  Progress/display messages (chunks,
+// markers, preview ImageData) are not emitted: they carry no results.
+// ---------------------------------------------------------------------------
+export function createWorkerHandler(post, { matrix2d = true, device = 0 } = {}) {
+  return (e) => {
+    const m = e && e.data !== undefined ? e.data : e;
+    switch (m.type) {
+      case WorkerMessageTypes.COMPUTE_GAUSSIAN_SCALE_SPACE:
+        post({ type: WorkerMessageTypes.RECEIVED_GAUSSIAN_SCALE_SPACE,
+          scaleSpace: computeGaussianScaleSpace({ input_image: m.inputImage, number_of_octaves: m.numberOfOctaves,
+            scales_per_octave: m.scalesPerOctave, min_blur_level: m.minBlurLevel, assumed_blur: m.assumedBlur,
+            chunk_size: m.chunkSize, matrix2d, device }) });
+        break;
+      case WorkerMessageTypes.COMPUTE_DIFFERENCE_OF_GAUSSIANS:
+        post({ type: WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIANS,
+          differenceOfGaussians: computeDifferenceOfGaussians(m.scaleSpace, 32, { device, matrix2d }) });
+        break;
+      case WorkerMessageTypes.FIND_CANDIDATE_KEYPOINTS:
+        post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINTS,
+          candidateKeypoints: findCandidateKeypoints({ ...m, device }) });
+        break;
+      case WorkerMessageTypes.REFINE_CANDIDATE_KEYPOINTS:
+        post({ type: WorkerMessageTypes.RECEIVED_REFINED_KEYPOINTS,
+          refinedKeypoints: refineCandidateKeypoints({ ...m, device }) });
+        break;
+      default:
+        console.log('sift worker received an unknown message:', m);
+    }
+  };
+}
+
+export const abiVersion = native.abiVersion();

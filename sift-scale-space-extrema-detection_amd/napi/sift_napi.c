@@ -1,0 +1,515 @@
+/*
+ * sift_napi.c -- Node N-API addon over the C ABI of libsift_hip.so.
+ *
+ * This is the FFI a maintainer of the reference (browser/Node JS) binds: a
+ * thin, zero-copy layer that hands ImageData-shaped Float32Array buffers to
+ * include/sift_hip.h and returns typed arrays.  The JS module ../js/sift.mjs
+ * builds the reference's call surface (src/worker.js / background.js) on it.
+ * Heavy calls exist in a synchronous form and, for the one-call detector, an
+ * async form on the libuv pool (napi_create_async_work) that resolves a
+ * Promise, so the JS thread is not blocked -- the role the reference's Web
+ * Worker plays.
+ */
+#define NAPI_VERSION 6
+#include <node_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/sift_hip.h"
+
+#define NAPI_CALL(env, call)                                              \
+  do {                                                                    \
+    if ((call) != napi_ok) {                                              \
+      napi_throw_error((env), NULL, "N-API call failed: " #call);        \
+      return NULL;                                                        \
+    }                                                                     \
+  } while (0)
+
+static napi_value throw_sift(napi_env env, struct sift_ctx *ctx, int rc, const char *what) {
+  char buf[512];
+  snprintf(buf, sizeof buf, "%s failed (%d): %s", what, rc, ctx ? sift_last_error(ctx) : "");
+  napi_value msg, err, code;
+  napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &msg);
+  napi_create_error(env, NULL, msg, &err);
+  napi_create_int32(env, rc, &code);
+  napi_set_named_property(env, err, "siftCode", code);
+  napi_throw(env, err);
+  return NULL;
+}
+
+static void ctx_finalize(napi_env env, void *data, void *hint) {
+  (void)env;
+  (void)hint;
+  if (data) sift_ctx_destroy((struct sift_ctx *)data);
+}
+
+static struct sift_ctx *get_ctx(napi_env env, napi_value v) {
+  void *p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, NULL, "expected a sift context");
+    return NULL;
+  }
+  return (struct sift_ctx *)p;
+}
+
+static int get_i32_prop(napi_env env, napi_value obj, const char *name, int def) {
+  bool has = false;
+  napi_value v;
+  int32_t r = def;
+  if (napi_has_named_property(env, obj, name, &has) == napi_ok && has &&
+      napi_get_named_property(env, obj, name, &v) == napi_ok) {
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_number) napi_get_value_int32(env, v, &r);
+  }
+  return r;
+}
+
+static double get_f64_prop(napi_env env, napi_value obj, const char *name, double def) {
+  bool has = false;
+  napi_value v;
+  double r = def;
+  if (napi_has_named_property(env, obj, name, &has) == napi_ok && has &&
+      napi_get_named_property(env, obj, name, &v) == napi_ok) {
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_number) napi_get_value_double(env, v, &r);
+  }
+  return r;
+}
+
+/* params object with the C field names (the JS module maps worker.js names). */
+static void read_params(napi_env env, napi_value obj, sift_params *p) {
+  sift_params_default(p);
+  p->num_octaves = get_i32_prop(env, obj, "num_octaves", p->num_octaves);
+  p->scales_per_octave = get_i32_prop(env, obj, "scales_per_octave", p->scales_per_octave);
+  p->min_blur = get_f64_prop(env, obj, "min_blur", p->min_blur);
+  p->assumed_blur = get_f64_prop(env, obj, "assumed_blur", p->assumed_blur);
+  p->min_interpixel_distance = get_f64_prop(env, obj, "min_interpixel_distance", p->min_interpixel_distance);
+  p->flags = get_i32_prop(env, obj, "flags", 0);
+}
+
+static void *typed_data(napi_env env, napi_value v, napi_typedarray_type want, size_t *len) {
+  bool is = false;
+  napi_is_typedarray(env, v, &is);
+  if (!is) return NULL;
+  napi_typedarray_type t;
+  size_t n;
+  void *data;
+  napi_value ab;
+  size_t off;
+  if (napi_get_typedarray_info(env, v, &t, &n, &data, &ab, &off) != napi_ok || t != want) return NULL;
+  if (len) *len = n;
+  return data;
+}
+
+static napi_value make_typed(napi_env env, napi_typedarray_type t, size_t n, size_t elem, void **data) {
+  napi_value ab, arr;
+  void *p = NULL;
+  if (napi_create_arraybuffer(env, n * elem, &p, &ab) != napi_ok) return NULL;
+  if (napi_create_typedarray(env, t, n, ab, 0, &arr) != napi_ok) return NULL;
+  if (data) *data = p;
+  return arr;
+}
+
+/* createContext(device) -> external */
+static napi_value js_create_context(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int32_t dev = 0;
+  if (argc > 0) napi_get_value_int32(env, argv[0], &dev);
+  struct sift_ctx *ctx = NULL;
+  int rc = sift_ctx_create(dev, &ctx);
+  if (rc) return throw_sift(env, NULL, rc, "sift_ctx_create (is a HIP device visible?)");
+  napi_value ext;
+  NAPI_CALL(env, napi_create_external(env, ctx, ctx_finalize, NULL, &ext));
+  return ext;
+}
+
+/* octaveDims(width, height, numOctaves) -> Int32Array(2*O) */
+static napi_value js_octave_dims(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int32_t w = 0, h = 0, o = 0;
+  napi_get_value_int32(env, argv[0], &w);
+  napi_get_value_int32(env, argv[1], &h);
+  napi_get_value_int32(env, argv[2], &o);
+  if (o < 1 || o > 64) {
+    napi_throw_range_error(env, NULL, "numOctaves out of range");
+    return NULL;
+  }
+  int32_t *d;
+  napi_value arr = make_typed(env, napi_int32_array, 2 * (size_t)o, 4, (void **)&d);
+  int rc = sift_octave_dims(w, h, o, d);
+  if (rc) return throw_sift(env, NULL, rc, "sift_octave_dims");
+  return arr;
+}
+
+/* buildScaleSpace(ctx, Float32Array img, width, height, params, Float64Array|null sigmas) */
+static napi_value js_build(napi_env env, napi_callback_info info) {
+  size_t argc = 6;
+  napi_value argv[6];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t n = 0;
+  const float *img = (const float *)typed_data(env, argv[1], napi_float32_array, &n);
+  int32_t w = 0, h = 0;
+  napi_get_value_int32(env, argv[2], &w);
+  napi_get_value_int32(env, argv[3], &h);
+  if (!img || (size_t)w * (size_t)h > n) {
+    napi_throw_type_error(env, NULL, "image must be a Float32Array of width*height gray values");
+    return NULL;
+  }
+  sift_params p;
+  read_params(env, argv[4], &p);
+  const double *sig = NULL;
+  if (argc > 5) sig = (const double *)typed_data(env, argv[5], napi_float64_array, NULL);
+  int rc = sift_build_scale_space(ctx, img, w, h, (size_t)w, &p, sig);
+  if (rc) return throw_sift(env, ctx, rc, "sift_build_scale_space");
+  return NULL;
+}
+
+/* getPlane(ctx, kind, octave, scale) -> Float32Array */
+static napi_value js_get_plane(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t kind = 0, o = 0, s = 0, rows = 0, cols = 0;
+  napi_get_value_int32(env, argv[1], &kind);
+  napi_get_value_int32(env, argv[2], &o);
+  napi_get_value_int32(env, argv[3], &s);
+  int rc = sift_get_dims(ctx, o, &rows, &cols);
+  if (rc) return throw_sift(env, ctx, rc, "sift_get_dims");
+  float *dst;
+  napi_value arr = make_typed(env, napi_float32_array, (size_t)rows * cols, 4, (void **)&dst);
+  rc = sift_get_plane(ctx, kind, o, s, dst, (size_t)rows * cols);
+  if (rc) return throw_sift(env, ctx, rc, "sift_get_plane");
+  return arr;
+}
+
+/* getDims(ctx, octave) -> [rows, cols] */
+static napi_value js_get_dims(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t o = 0, r = 0, c = 0;
+  napi_get_value_int32(env, argv[1], &o);
+  int rc = sift_get_dims(ctx, o, &r, &c);
+  if (rc) return throw_sift(env, ctx, rc, "sift_get_dims");
+  napi_value arr, a, b;
+  napi_create_array_with_length(env, 2, &arr);
+  napi_create_int32(env, r, &a);
+  napi_create_int32(env, c, &b);
+  napi_set_element(env, arr, 0, a);
+  napi_set_element(env, arr, 1, b);
+  return arr;
+}
+
+/* loadDog / loadScaleSpace(ctx, Float32Array flat, width, height, params) */
+static napi_value load_common(napi_env env, napi_callback_info info, int which) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  const float *flat = (const float *)typed_data(env, argv[1], napi_float32_array, NULL);
+  if (!flat) {
+    napi_throw_type_error(env, NULL, "planes must be a Float32Array");
+    return NULL;
+  }
+  int32_t w = 0, h = 0;
+  napi_get_value_int32(env, argv[2], &w);
+  napi_get_value_int32(env, argv[3], &h);
+  sift_params p;
+  read_params(env, argv[4], &p);
+  int rc = which ? sift_load_scale_space(ctx, flat, w, h, &p) : sift_load_dog(ctx, flat, w, h, &p);
+  if (rc) return throw_sift(env, ctx, rc, which ? "sift_load_scale_space" : "sift_load_dog");
+  return NULL;
+}
+static napi_value js_load_dog(napi_env env, napi_callback_info info) { return load_common(env, info, 0); }
+static napi_value js_load_ss(napi_env env, napi_callback_info info) { return load_common(env, info, 1); }
+
+/* findExtrema(ctx) -> {ints: Int32Array(4n) [o,s,x,y], values: Float64Array(n), lowContrast} */
+static napi_value js_find_extrema(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t n = 0, low = 0;
+  int rc = sift_find_extrema(ctx, NULL, 0, &n, &low);
+  if (rc) return throw_sift(env, ctx, rc, "sift_find_extrema");
+  sift_extremum *tmp = (sift_extremum *)malloc(sizeof(sift_extremum) * (n ? n : 1));
+  rc = sift_copy_candidates(ctx, tmp, n, &n);
+  if (rc) {
+    free(tmp);
+    return throw_sift(env, ctx, rc, "sift_copy_candidates");
+  }
+  int32_t *ints;
+  double *vals;
+  napi_value ia = make_typed(env, napi_int32_array, 4 * n, 4, (void **)&ints);
+  napi_value va = make_typed(env, napi_float64_array, n, 8, (void **)&vals);
+  for (size_t i = 0; i < n; ++i) {
+    ints[4 * i] = tmp[i].octave;
+    ints[4 * i + 1] = tmp[i].scale;
+    ints[4 * i + 2] = tmp[i].x;
+    ints[4 * i + 3] = tmp[i].y;
+    vals[i] = tmp[i].value;
+  }
+  free(tmp);
+  napi_value out, lv;
+  napi_create_object(env, &out);
+  napi_set_named_property(env, out, "ints", ia);
+  napi_set_named_property(env, out, "values", va);
+  napi_create_double(env, (double)low, &lv);
+  napi_set_named_property(env, out, "lowContrast", lv);
+  return out;
+}
+
+/* setCandidates(ctx, Int32Array(4n) [o,s,x,y], Float64Array(n)) */
+static napi_value js_set_candidates(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t ni = 0, nv = 0;
+  const int32_t *ints = (const int32_t *)typed_data(env, argv[1], napi_int32_array, &ni);
+  const double *vals = (const double *)typed_data(env, argv[2], napi_float64_array, &nv);
+  if (!ints || !vals || ni != 4 * nv) {
+    napi_throw_type_error(env, NULL, "expected Int32Array(4n) and Float64Array(n)");
+    return NULL;
+  }
+  sift_extremum *c = (sift_extremum *)malloc(sizeof(sift_extremum) * (nv ? nv : 1));
+  for (size_t i = 0; i < nv; ++i) {
+    c[i].octave = ints[4 * i];
+    c[i].scale = ints[4 * i + 1];
+    c[i].x = ints[4 * i + 2];
+    c[i].y = ints[4 * i + 3];
+    c[i].value = vals[i];
+  }
+  int rc = sift_set_candidates(ctx, c, nv);
+  free(c);
+  if (rc) return throw_sift(env, ctx, rc, "sift_set_candidates");
+  return NULL;
+}
+
+/* setRefineParams(ctx, minBlurLevel, minInterpixelDistance) */
+static napi_value js_refine_params(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  double mb = 0.8, mid = 0.5;
+  napi_get_value_double(env, argv[1], &mb);
+  napi_get_value_double(env, argv[2], &mid);
+  int rc = sift_refine_params(ctx, mb, mid);
+  if (rc) return throw_sift(env, ctx, rc, "sift_refine_params");
+  return NULL;
+}
+
+static napi_value keypoints_to_js(napi_env env, struct sift_ctx *ctx, size_t n, size_t singular) {
+  sift_keypoint *tmp = (sift_keypoint *)malloc(sizeof(sift_keypoint) * (n ? n : 1));
+  int rc = sift_copy_keypoints(ctx, tmp, n, &n);
+  if (rc) {
+    free(tmp);
+    return throw_sift(env, ctx, rc, "sift_copy_keypoints");
+  }
+  int32_t *ints;
+  double *d;
+  napi_value ia = make_typed(env, napi_int32_array, 4 * n, 4, (void **)&ints);
+  napi_value da = make_typed(env, napi_float64_array, 4 * n, 8, (void **)&d);
+  for (size_t i = 0; i < n; ++i) {
+    ints[4 * i] = tmp[i].octave;
+    ints[4 * i + 1] = tmp[i].scale_level;
+    ints[4 * i + 2] = tmp[i].local_x;
+    ints[4 * i + 3] = tmp[i].local_y;
+    d[4 * i] = tmp[i].abs_sigma;
+    d[4 * i + 1] = tmp[i].abs_x;
+    d[4 * i + 2] = tmp[i].abs_y;
+    d[4 * i + 3] = tmp[i].interp_value;
+  }
+  free(tmp);
+  napi_value out, sv;
+  napi_create_object(env, &out);
+  napi_set_named_property(env, out, "ints", ia);      /* octave, scaleLevel, localX, localY */
+  napi_set_named_property(env, out, "doubles", da);   /* absoluteSigma, absoluteX, absoluteY, interpolatedValue */
+  napi_create_double(env, (double)singular, &sv);
+  napi_set_named_property(env, out, "singular", sv);
+  return out;
+}
+
+/* refine(ctx) -> {ints, doubles, singular} (singular > 0: caller mirrors the reference's TypeError) */
+static napi_value js_refine(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t n = 0, sing = 0;
+  int rc = sift_refine(ctx, NULL, 0, &n, &sing);
+  if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_refine");
+  return keypoints_to_js(env, ctx, n, sing);
+}
+
+/* detect(ctx, img, width, height, params) -> {ints, doubles, singular} */
+static napi_value js_detect(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t len = 0;
+  const float *img = (const float *)typed_data(env, argv[1], napi_float32_array, &len);
+  int32_t w = 0, h = 0;
+  napi_get_value_int32(env, argv[2], &w);
+  napi_get_value_int32(env, argv[3], &h);
+  if (!img || (size_t)w * (size_t)h > len) {
+    napi_throw_type_error(env, NULL, "image must be a Float32Array of width*height gray values");
+    return NULL;
+  }
+  sift_params p;
+  read_params(env, argv[4], &p);
+  size_t n = 0;
+  int rc = sift_detect(ctx, img, w, h, (size_t)w, &p, NULL, 0, &n);
+  if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_detect");
+  size_t sing = 0;
+  sift_last_counts(ctx, NULL, NULL, NULL, &sing, NULL);
+  return keypoints_to_js(env, ctx, n, sing);
+}
+
+/* ---- detectAsync: the one-call path on the libuv pool, returns a Promise ---- */
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref img_ref;
+  napi_ref ctx_ref;
+  struct sift_ctx *ctx;
+  const float *img;
+  int w, h, rc;
+  sift_params p;
+  size_t n;
+} detect_job;
+
+static void detect_execute(napi_env env, void *data) {
+  (void)env;
+  detect_job *j = (detect_job *)data;
+  j->rc = sift_detect(j->ctx, j->img, j->w, j->h, (size_t)j->w, &j->p, NULL, 0, &j->n);
+}
+
+static void detect_complete(napi_env env, napi_status status, void *data) {
+  detect_job *j = (detect_job *)data;
+  if (status == napi_ok && (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR)) {
+    size_t sing = 0;
+    sift_last_counts(j->ctx, NULL, NULL, NULL, &sing, NULL);
+    napi_value res = keypoints_to_js(env, j->ctx, j->n, sing);
+    if (res) {
+      napi_resolve_deferred(env, j->deferred, res);
+    } else {
+      napi_value exc;
+      napi_get_and_clear_last_exception(env, &exc);
+      napi_reject_deferred(env, j->deferred, exc);
+    }
+  } else {
+    char buf[512];
+    snprintf(buf, sizeof buf, "sift_detect failed (%d): %s", j->rc, sift_last_error(j->ctx));
+    napi_value msg, err;
+    napi_create_string_utf8(env, buf, NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, j->deferred, err);
+  }
+  napi_delete_reference(env, j->img_ref);
+  napi_delete_reference(env, j->ctx_ref);
+  napi_delete_async_work(env, j->work);
+  free(j);
+}
+
+static napi_value js_detect_async(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t len = 0;
+  const float *img = (const float *)typed_data(env, argv[1], napi_float32_array, &len);
+  int32_t w = 0, h = 0;
+  napi_get_value_int32(env, argv[2], &w);
+  napi_get_value_int32(env, argv[3], &h);
+  if (!img || (size_t)w * (size_t)h > len) {
+    napi_throw_type_error(env, NULL, "image must be a Float32Array of width*height gray values");
+    return NULL;
+  }
+  detect_job *j = (detect_job *)calloc(1, sizeof(detect_job));
+  j->ctx = ctx;
+  j->img = img;
+  j->w = w;
+  j->h = h;
+  read_params(env, argv[4], &j->p);
+  napi_value promise, name;
+  NAPI_CALL(env, napi_create_promise(env, &j->deferred, &promise));
+  NAPI_CALL(env, napi_create_reference(env, argv[1], 1, &j->img_ref));  /* keep the buffer alive */
+  NAPI_CALL(env, napi_create_reference(env, argv[0], 1, &j->ctx_ref));
+  napi_create_string_utf8(env, "sift_detect", NAPI_AUTO_LENGTH, &name);
+  NAPI_CALL(env, napi_create_async_work(env, NULL, name, detect_execute, detect_complete, j, &j->work));
+  NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  return promise;
+}
+
+static napi_value js_counts(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t v[5] = {0, 0, 0, 0, 0};
+  sift_last_counts(ctx, &v[0], &v[1], &v[2], &v[3], &v[4]);
+  const char *names[5] = {"candidates", "lowContrast", "keypoints", "singular", "exact"};
+  napi_value out;
+  napi_create_object(env, &out);
+  for (int i = 0; i < 5; ++i) {
+    napi_value x;
+    napi_create_double(env, (double)v[i], &x);
+    napi_set_named_property(env, out, names[i], x);
+  }
+  return out;
+}
+
+static napi_value js_abi_version(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value v;
+  napi_create_int32(env, sift_abi_version(), &v);
+  return v;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"abiVersion", 0, js_abi_version, 0, 0, 0, napi_enumerable, 0},
+      {"createContext", 0, js_create_context, 0, 0, 0, napi_enumerable, 0},
+      {"octaveDims", 0, js_octave_dims, 0, 0, 0, napi_enumerable, 0},
+      {"buildScaleSpace", 0, js_build, 0, 0, 0, napi_enumerable, 0},
+      {"getPlane", 0, js_get_plane, 0, 0, 0, napi_enumerable, 0},
+      {"getDims", 0, js_get_dims, 0, 0, 0, napi_enumerable, 0},
+      {"loadDog", 0, js_load_dog, 0, 0, 0, napi_enumerable, 0},
+      {"loadScaleSpace", 0, js_load_ss, 0, 0, 0, napi_enumerable, 0},
+      {"findExtrema", 0, js_find_extrema, 0, 0, 0, napi_enumerable, 0},
+      {"setCandidates", 0, js_set_candidates, 0, 0, 0, napi_enumerable, 0},
+      {"refine", 0, js_refine, 0, 0, 0, napi_enumerable, 0},
+      {"setRefineParams", 0, js_refine_params, 0, 0, 0, napi_enumerable, 0},
+      {"detect", 0, js_detect, 0, 0, 0, napi_enumerable, 0},
+      {"detectAsync", 0, js_detect_async, 0, 0, 0, napi_enumerable, 0},
+      {"counts", 0, js_counts, 0, 0, 0, napi_enumerable, 0},
+  };
+  napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

@@ -34,7 +34,7 @@ ABI_SYMBOLS = (
     "sift_last_error", "sift_schedule", "sift_octave_dims", "sift_build_scale_space",
     "sift_build_scale_space_device", "sift_get_dims", "sift_get_blur_level", "sift_get_plane",
     "sift_load_dog", "sift_load_scale_space", "sift_find_extrema", "sift_refine",
-    "sift_set_candidates", "sift_copy_candidates", "sift_copy_keypoints",
+    "sift_set_candidates", "sift_refine_params", "sift_copy_candidates", "sift_copy_keypoints",
     "sift_copy_keypoints_device", "sift_detect", "sift_detect_device", "sift_last_counts",
     "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
 )
@@ -119,6 +119,7 @@ def lib():
         "sift_find_extrema": (ctypes.c_int, [vp, vp, sz, szp, szp]),
         "sift_refine": (ctypes.c_int, [vp, vp, sz, szp, szp]),
         "sift_set_candidates": (ctypes.c_int, [vp, vp, sz]),
+        "sift_refine_params": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double]),
         "sift_copy_candidates": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_copy_keypoints": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_copy_keypoints_device": (ctypes.c_int, [vp, vp, sz, szp]),
@@ -276,6 +277,10 @@ class Context:
         self._check(self._L.sift_copy_keypoints(self._h, out.ctypes.data_as(ctypes.c_void_p), out.shape[0],
                                                 ctypes.byref(n)), "sift_copy_keypoints")
         return out[:n.value]
+
+    def refine_params(self, min_blur_level, min_interpixel_distance=0.5):
+        self._check(self._L.sift_refine_params(self._h, float(min_blur_level), float(min_interpixel_distance)),
+                    "sift_refine_params")
 
     def set_candidates(self, cand):
         c = np.ascontiguousarray(cand, dtype=EXTREMUM_DTYPE)
