@@ -267,6 +267,21 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
       for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
       oc.rad[s] = r;
       oc.rmax = std::max(oc.rmax, r);
+      if (o == 0) {
+        // Folded octave-0 taps (k_gauss_o0): fw_e[k] = sum of w_i with
+        // floor((e+i-r)/2) == k, summed in increasing i.
+        const double* wv = &w[oc.wofs[s]];
+        std::vector<double> taps(wv, wv + 2 * r + 1);
+        for (int e = 0; e < 2; ++e) {
+          const int kmin = fold_kmin(e, r);
+          std::vector<double> f(r + 1, 0.0);
+          for (int i = 0; i <= 2 * r; ++i) f[((e + i - r) >> 1) - kmin] += taps[i];
+          for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
+          P.f0ofs[e][s] = (int)w.size();
+          for (double v : f) w.push_back(v);
+          for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
+        }
+      }
     }
   }
   if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");

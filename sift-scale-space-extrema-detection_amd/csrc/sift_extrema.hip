@@ -7,14 +7,14 @@
 // it is a low-contrast extremum.  Output order is the reference's: octave,
 // scale, then raster (y, x).
 //
-// k_extrema: one wave per (scale, band of kXR rows), sweeping 64-column words
-// left to right.  Per word each lane loads its column of the three DoG planes
-// (rows y-1 .. y+kXR), takes x-1 / x+1 from its neighbours with DPP wave
-// shifts (word edges from one extra load), reduces the 26 neighbours with
-// max3/min3, and ballots the candidate mask of the 64 pixels straight into a
-// bitmap word [s][y][x/64].  Row popcounts are exact per wave (no atomics).
-// k_emit expands the bitmap in order after an exclusive scan of the row
-// counts -- the candidate list comes out sorted without a sort.
+// k_extrema: one block per (64-column word, strip of kXStrip rows), one wave
+// per DoG scale, sliding a 3-row window down the strip.  Each lane loads its
+// column of the three DoG planes, takes x-1 / x+1 from its neighbours with
+// DPP wave shifts (word edges from one extra load), reduces the 26
+// neighbours with max3/min3, and ballots the candidate mask of the 64 pixels
+// straight into a bitmap word [s][y][x/64] plus a per-row popcount.  k_emit
+// expands the bitmap in order after an exclusive scan of the row counts --
+// the candidate list comes out sorted without a sort.
 //
 // The planes are fp32 roundings of fp64 values.  Rounding is monotone, so an
 // fp32 comparison decides the fp64 one unless two fp32 values tie; ties and
@@ -51,94 +51,97 @@ __device__ __forceinline__ float from_right(float v, float edge) {
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(a, fmaxf(b, c)); }
 __device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(a, fminf(b, c)); }
 
-__global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
+// One block per (64-column word, strip of kXStrip rows); wave s-1 of the
+// block scans DoG scale s.  The S waves of a block read overlapping planes
+// at the same rows, so each plane streams from HBM about once (L1/L2 reuse).
+__global__ __launch_bounds__(576) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
   const Octave& oc = P.oct[L.o];
-  const int h = oc.h, w = oc.w, S = P.S;
+  const int h = oc.h, w = oc.w;
   const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave id
-  const int s = 1 + gw % S;                           // scale fastest: trios of one band run together
-  const int y0 = 1 + (gw / S) * kXR;
-  if (y0 > h - 2) return;                              // wave-uniform
-  const int ny = min(kXR, h - 1 - y0);                 // rows y0 .. y0+ny-1 (<= h-2)
+  const int s = 1 + (threadIdx.x >> 6);
+  const int xw = blockIdx.x;
+  const int y0 = 1 + blockIdx.y * kXStrip;
+  const int y1 = min(h - 2, y0 + kXStrip - 1);
   const long long plane = (long long)h * w;
   const float* __restrict__ D = P.dog + oc.dog_off;
-  const float* Dp[3] = {D + (s - 1) * plane, D + s * plane, D + (s + 1) * plane};
+  const float* __restrict__ Dm = D + (s - 1) * plane;
+  const float* __restrict__ Dc = D + s * plane;
+  const float* __restrict__ Dq = D + (s + 1) * plane;
   const double T = P.pix_thr;
-  unsigned rowcnt[kXR];
-#pragma unroll
-  for (int r = 0; r < kXR; ++r) rowcnt[r] = 0;
+  const int x = xw * 64 + lane;
+  const int xc = min(x, w - 1);
+  const bool is_edge = lane == 0 || lane == 63;
+  const int xe = clampi(lane == 0 ? x - 1 : x + 1, 0, w - 1);
+  const bool col_ok = x >= 1 && x <= w - 2;
   unsigned low = 0;
-  const int edge_dx = lane == 0 ? -1 : 1;
 
-  for (int xw = 0; xw < L.nw; ++xw) {
-    const int x = xw * 64 + lane;
-    const int xc = min(x, w - 1);
-    const int xe = clampi(x + edge_dx, 0, w - 1);
-    // Per plane and row: 3-wide max / min; centre plane also the 2-wide
-    // (x-1, x+1) max / min and the value itself.
-    float hmx[3][kXR + 2], hmn[3][kXR + 2];
-    float emx[kXR + 2], emn[kXR + 2], cv[kXR + 2];
+  // Sliding 3-row window: per plane the 3-wide max/min of rows y-1, y, y+1;
+  // the centre plane also keeps the 2-wide (x-1, x+1) max/min and the value.
+  float mx[3][3], mn[3][3], emx[3], emn[3], cv[3];
+  auto load_row = [&](int yy, int slot) {
+    const long long row = (long long)yy * w;
+    const float* planes[3] = {Dm, Dc, Dq};
 #pragma unroll
-    for (int r = 0; r < kXR + 2; ++r) {
-      const int yy = min(y0 - 1 + r, h - 1);
-      const long long row = (long long)yy * w;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const float v = Dp[q][row + xc];
-        const float e = Dp[q][row + xe];
-        const float vl = from_left(v, e), vr = from_right(v, e);
-        hmx[q][r] = max3f(vl, v, vr);
-        hmn[q][r] = min3f(vl, v, vr);
-        if (q == 1) {
-          emx[r] = fmaxf(vl, vr);
-          emn[r] = fminf(vl, vr);
-          cv[r] = v;
-        }
+    for (int q = 0; q < 3; ++q) {
+      const float v = planes[q][row + xc];
+      float e = v;
+      if (is_edge) e = planes[q][row + xe];
+      const float vl = from_left(v, e), vr = from_right(v, e);
+      mx[q][slot] = max3f(vl, v, vr);
+      mn[q][slot] = min3f(vl, v, vr);
+      if (q == 1) {
+        emx[slot] = fmaxf(vl, vr);
+        emn[slot] = fminf(vl, vr);
+        cv[slot] = v;
       }
     }
-    const bool col_ok = x >= 1 && x <= w - 2;
-#pragma unroll
-    for (int r = 1; r <= kXR; ++r) {
-      if (r > ny) break;  // wave-uniform
-      const float v = cv[r];
-      const float nmax = max3f(max3f(hmx[0][r - 1], hmx[0][r], hmx[0][r + 1]),
-                               max3f(hmx[2][r - 1], hmx[2][r], hmx[2][r + 1]),
-                               max3f(hmx[1][r - 1], hmx[1][r + 1], emx[r]));
-      const float nmin = min3f(min3f(hmn[0][r - 1], hmn[0][r], hmn[0][r + 1]),
-                               min3f(hmn[2][r - 1], hmn[2][r], hmn[2][r + 1]),
-                               min3f(hmn[1][r - 1], hmn[1][r + 1], emn[r]));
-      const bool possible = v >= nmax || v <= nmin;    // no neighbour strictly beyond v
-      const bool certain = v > nmax || v < nmin;       // strict in fp32 => strict in fp64
-      bool ext, tie;
-      if (L.exact_planes) { ext = certain; tie = false; }
-      else { ext = possible; tie = !certain; }
-      ext = ext && col_ok;
-      const double av = fabs((double)v);
-      bool low_certain, contrast_amb = false;
-      if (L.exact_planes) {
-        low_certain = av < T;
-      } else {
-        const double e = av * 0x1p-24 + 1e-300;  // |v - v_fp64| <= ulp/2 <= |v| 2^-24
-        low_certain = av + e < T;
-        contrast_amb = !low_certain && av - e < T;
-      }
-      const bool count_low = ext && low_certain && !tie;
-      const bool bit = ext && !count_low;
-      low += count_low ? 1u : 0u;
-      const unsigned long long word = __ballot(bit);
-      const int y = y0 + r - 1;
-      if (lane == 0) L.bitmap[((long long)(s - 1) * h + y) * L.nw + xw] = word;
-      rowcnt[r - 1] += (unsigned)__popcll(word);
-      const bool amb = bit && (tie || contrast_amb);
+  };
+  load_row(y0 - 1, 0);
+  load_row(y0, 1);
+  for (int y = y0; y <= y1; ++y) {
+    load_row(y + 1, 2);
+    const float v = cv[1];
+    const float nmax = max3f(max3f(mx[0][0], mx[0][1], mx[0][2]), max3f(mx[2][0], mx[2][1], mx[2][2]),
+                             max3f(mx[1][0], mx[1][2], emx[1]));
+    const float nmin = min3f(min3f(mn[0][0], mn[0][1], mn[0][2]), min3f(mn[2][0], mn[2][1], mn[2][2]),
+                             min3f(mn[1][0], mn[1][2], emn[1]));
+    const bool possible = v >= nmax || v <= nmin;  // no neighbour strictly beyond v
+    const bool certain = v > nmax || v < nmin;     // strict in fp32 => strict in fp64
+    bool ext, tie;
+    if (L.exact_planes) { ext = certain; tie = false; }
+    else { ext = possible; tie = !certain; }
+    ext = ext && col_ok;
+    const double av = fabs((double)v);
+    bool low_certain, contrast_amb = false;
+    if (L.exact_planes) {
+      low_certain = av < T;
+    } else {
+      const double e = av * 0x1p-24 + 1e-300;  // |v - v_fp64| <= ulp/2 <= |v| 2^-24
+      low_certain = av + e < T;
+      contrast_amb = !low_certain && av - e < T;
+    }
+    const bool count_low = ext && low_certain && !tie;
+    const bool bit = ext && !count_low;
+    low += count_low ? 1u : 0u;
+    const unsigned long long word = __ballot(bit);
+    if (lane == 0) {
+      L.bitmap[((long long)(s - 1) * h + y) * L.nw + xw] = word;
+      if (word) atomicAdd(&L.rowcount[(s - 1) * h + y], (unsigned)__popcll(word));
+    }
+    const bool amb = bit && (tie || contrast_amb);
+    if (__ballot(amb)) {  // rare
       const unsigned slot = wave_append(amb, &L.counters[0]);
       if (amb && slot < L.amb_cap)
         L.amb_keys[slot] = oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w + (unsigned)x;
     }
-  }
-  if (lane == 0) {
 #pragma unroll
-    for (int r = 0; r < kXR; ++r)
-      if (r < ny) L.rowcount[(s - 1) * h + y0 + r] = rowcnt[r];
+    for (int q = 0; q < 3; ++q) {
+      mx[q][0] = mx[q][1]; mx[q][1] = mx[q][2];
+      mn[q][0] = mn[q][1]; mn[q][1] = mn[q][2];
+    }
+    emx[0] = emx[1]; emx[1] = emx[2];
+    emn[0] = emn[1]; emn[1] = emn[2];
+    cv[0] = cv[1]; cv[1] = cv[2];
   }
   // wave sum of the low-contrast count, one atomic per wave
 #pragma unroll
@@ -226,9 +229,8 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
 hipError_t launch_extrema(const Pyramid& P, const ExtremaLaunch& L, hipStream_t st) {
   const Octave& oc = P.oct[L.o];
   if (oc.h < 3 || oc.w < 3 || P.S < 1) return hipSuccess;  // no interior pixels
-  const int bands = (oc.h - 2 + kXR - 1) / kXR;
-  const int waves = bands * P.S;
-  hipLaunchKernelGGL(k_extrema, dim3((waves + 3) / 4), dim3(256), 0, st, P, L);
+  const int strips = (oc.h - 2 + kXStrip - 1) / kXStrip;
+  hipLaunchKernelGGL(k_extrema, dim3(L.nw, strips), dim3(64 * P.S), 0, st, P, L);
   return hipGetLastError();
 }
 

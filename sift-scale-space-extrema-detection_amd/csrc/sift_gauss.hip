@@ -135,6 +135,125 @@ __global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussL
   }
 }
 
+// Octave 0, folded.  The octave-0 base is the 2x nearest-neighbour upsample
+// of the input (background.js:84), so B[y][x] = I[y>>1][x>>1] and clamping
+// commutes with the halving.  The horizontal sum depends on y only through
+// q = y>>1, and both passes fold their 2r+1 taps onto r+1 input pixels with
+// parity-dependent weights (sift_common.h, f0ofs): per output pixel and
+// scale about (r+1)/2 + (r+4) FMAs instead of 2(2r+1), and the tile stages
+// only the fp32 input region.  Same outputs as k_gauss_dog otherwise.
+__global__ __launch_bounds__(256) void k_gauss_o0(const Pyramid P, const GaussLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Octave& oc = P.oct[0];
+  const int h = oc.h, w = oc.w, H = P.H, W = P.W;
+  const int cR = fold_half(oc.rmax);
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+  const int p0 = x0 >> 1, a0 = y0 >> 1;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+
+  // Input region: rows qlo_all..qhi_all (distinct, clamped), columns
+  // p0-cR .. p0+31+cR with replicated edges, as fp64.
+  const int qlo_all = max(0, a0 - cR), qhi_all = min(H - 1, a0 + kTY / 2 - 1 + cR);
+  const int IW = kTX / 2 + 2 * cR;
+  double* sI = smem;
+  double* sQ = smem + (size_t)(qhi_all - qlo_all + 1) * IW;
+  {
+    const float* __restrict__ img = P.img;
+    const int n = (qhi_all - qlo_all + 1) * IW;
+    for (int idx = tid; idx < n; idx += 256) {
+      const int rr = idx / IW, cc = idx - rr * IW;
+      sI[idx] = (double)img[(long long)(qlo_all + rr) * P.img_stride + clampi(p0 - cR + cc, 0, W - 1)];
+    }
+  }
+  __syncthreads();
+
+  const long long plane = (long long)h * w;
+  const int x = x0 + lane;
+  const int A = a0 + (wv * kVT) / 2;  // first input row of this wave's 8 output rows
+  double lprev[kVT];
+#pragma unroll
+  for (int t = 0; t < kVT; ++t) lprev[t] = 0.0;
+
+  for (int s = 0; s < P.NS; ++s) {
+    const int r = oc.rad[s], c = fold_half(r);
+    const int kmin0 = fold_kmin(0, r), kmin1 = fold_kmin(1, r);
+    const cdouble* f0 = (const cdouble*)(P.wts + P.f0ofs[0][s]);
+    const cdouble* f1 = (const cdouble*)(P.wts + P.f0ofs[1][s]);
+    const int qlo = max(0, a0 - c), qhi = min(H - 1, a0 + kTY / 2 - 1 + c);
+    const int nq = qhi - qlo + 1;
+
+    // Horizontal: hq[q][2p+e] = sum_j fw_e[j] I[q][clamp(p + kmin_e + j)].
+    // A unit is (row pair, parity): lanes 0-31 take row 2*pi, 32-63 row
+    // 2*pi+1, column pair p = lane & 31; units u and u+4 share a parity, so
+    // taps stay wave-uniform and two rows accumulate independently.
+    {
+      const int p = lane & 31, half = lane >> 5;
+      const int units = ((nq + 1) >> 1) * 2;
+      for (int u = wv; u < units; u += 8) {
+        const int e = u & 1;
+        const cdouble* fw = e ? f1 : f0;
+        const int kmin = e ? kmin1 : kmin0;
+        const int qa = qlo + 2 * (u >> 1) + half;
+        const int u2 = u + 4;
+        const bool has2 = u2 < units;
+        const int qb = qlo + 2 * (u2 >> 1) + half;
+        const int qa_c = min(qa, qhi), qb_c = min(qb, qhi);
+        const double* ra = sI + (size_t)(qa_c - qlo_all) * IW + p + kmin + cR;
+        const double* rb = sI + (size_t)(qb_c - qlo_all) * IW + p + kmin + cR;
+        double a = 0.0, b = 0.0;
+        for (int j = 0; j <= r; ++j) {
+          const double fj = fw[j];
+          a = fma(fj, ra[j], a);
+          b = fma(fj, rb[j], b);
+        }
+        if (qa <= qhi) sQ[(qa - qlo) * kTX + 2 * p + e] = a;
+        if (has2 && qb <= qhi) sQ[(qb - qlo) * kTX + 2 * p + e] = b;
+      }
+    }
+    __syncthreads();
+
+    // Vertical: L[2a+e][x] = sum_k fw_e[k] hq[clamp(a+k)][x] for a = A+m,
+    // m = 0..3; strip row j holds input row clamp(A - c + j).  Zero-padded
+    // taps keep each output's fma sequence k = kmin_e .. kmax_e.
+    double acc[kVT];
+#pragma unroll
+    for (int t = 0; t < kVT; ++t) acc[t] = 0.0;
+    for (int j = 0; j < 2 * c + 4; ++j) {
+      const int qq = clampi(A - c + j, 0, H - 1) - qlo;
+      const double v = sQ[qq * kTX + lane];
+#pragma unroll
+      for (int m = 0; m < kVT / 2; ++m) {
+        const int k = j - c - m;
+        acc[2 * m] = fma(f0[k - kmin0], v, acc[2 * m]);
+        acc[2 * m + 1] = fma(f1[k - kmin1], v, acc[2 * m + 1]);
+      }
+    }
+    __syncthreads();
+
+    if (x < w) {
+#pragma unroll
+      for (int t = 0; t < kVT; ++t) {
+        const int y = y0 + wv * kVT + t;
+        if (y < h) {
+          const long long pp = (long long)y * w + x;
+          if (L.gauss) L.gauss[s * plane + pp] = (float)acc[t];
+          if (s > 0) L.dog[(s - 1) * plane + pp] = (float)(lprev[t] - acc[t]);
+          if (s == P.S && L.next_seed && !(y & 1) && !(x & 1))
+            L.next_seed[(long long)(y >> 1) * L.next_w + (x >> 1)] = acc[t];
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < kVT; ++t) lprev[t] = acc[t];
+  }
+}
+
+size_t gauss_o0_lds_bytes(const Pyramid& P) {
+  const int cR = fold_half(P.oct[0].rmax);
+  const int rows = std::min(P.H, kTY / 2 + 2 * cR);
+  return sizeof(double) * (size_t)rows * ((kTX / 2 + 2 * cR) + kTX);
+}
+
 // DoG from a caller-supplied fp32 Gaussian pyramid (foreign scale space):
 // D[t] = L[t] - L[t+1] in fp64 (exact for fp32 operands), rounded once.
 __global__ __launch_bounds__(256) void k_dog_from_gauss(const float* __restrict__ g,
@@ -169,9 +288,14 @@ hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t 
     set_lds_attr<true, false>();
     set_lds_attr<false, true>();
     set_lds_attr<false, false>();
+    (void)hipFuncSetAttribute((const void*)k_gauss_o0, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const bool o0 = L.o == 0;
+  if (o0 && !L.unfolded) {
+    hipLaunchKernelGGL(k_gauss_o0, grid, dim3(256), gauss_o0_lds_bytes(P), st, P, L);
+    return hipGetLastError();
+  }
   if (L.base_lds && o0) hipLaunchKernelGGL((k_gauss_dog<true, true>), grid, dim3(256), lds, st, P, L);
   else if (L.base_lds) hipLaunchKernelGGL((k_gauss_dog<true, false>), grid, dim3(256), lds, st, P, L);
   else if (o0) hipLaunchKernelGGL((k_gauss_dog<false, true>), grid, dim3(256), lds, st, P, L);
