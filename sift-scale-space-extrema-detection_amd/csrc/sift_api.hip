@@ -267,27 +267,12 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
       for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
       oc.rad[s] = r;
       oc.rmax = std::max(oc.rmax, r);
-      if (o == 0) {
-        // Folded octave-0 taps (k_gauss_o0): fw_e[k] = sum of w_i with
-        // floor((e+i-r)/2) == k, summed in increasing i.
-        const double* wv = &w[oc.wofs[s]];
-        std::vector<double> taps(wv, wv + 2 * r + 1);
-        for (int e = 0; e < 2; ++e) {
-          const int kmin = fold_kmin(e, r);
-          std::vector<double> f(r + 1, 0.0);
-          for (int i = 0; i <= 2 * r; ++i) f[((e + i - r) >> 1) - kmin] += taps[i];
-          for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
-          P.f0ofs[e][s] = (int)w.size();
-          for (double v : f) w.push_back(v);
-          for (int z = 0; z < kWPad; ++z) w.push_back(0.0);
-        }
-      }
     }
   }
   if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");
   // LDS feasibility of the Gaussian kernel (strip of min(h, 32+2R) fp64 rows).
   for (int o = 0; o < O; ++o)
-    if (gauss_lds_bytes(P.oct[o], false) > 160 * 1024)
+    if (gauss_lds_bytes(P.oct[o]) > 160 * 1024)
       return set_err(ctx, SIFT_E_UNSUPPORTED, "blur radius too large for one LDS strip");
   if (need_weights) {
     if (ctx->wts.ensure(w.size() * sizeof(double)) != hipSuccess)
@@ -344,7 +329,6 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.dog = ctx->dog.as<float>() + oc.dog_off;
     L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off : nullptr;
     L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : 0;
-    L.base_lds = gauss_lds_bytes(oc, true) <= 112 * 1024 ? 1 : 0;
     HIPCHK(launch_gauss_dog(P, L, ctx->stream));
   }
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));

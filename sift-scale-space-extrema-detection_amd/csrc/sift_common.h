@@ -44,16 +44,8 @@ struct Pyramid {
   const float* dog;
   double pix_thr;        // 0.8 * thr   (sift.js:285-294)
   double thr;            // thr         (background.js:572)
-  // Octave 0 is the 2x nearest-neighbour upsample of the input, so its taps
-  // fold pairwise onto input pixels: for output parity e the folded vector
-  // fw_e[k], k = floor((e-r)/2) .. floor((e+r)/2), sums the w_i with
-  // floor((e+i-r)/2) == k.  f0ofs[e][s] = offset of fw_e[kmin_e] in wts.
-  int f0ofs[2][kMaxScales];
   Octave oct[kMaxOctaves];
 };
-
-__host__ __device__ __forceinline__ int fold_kmin(int e, int r) { return (e - r) >> 1; }  // floor((e-r)/2)
-__host__ __device__ __forceinline__ int fold_half(int r) { return (r + 1) >> 1; }        // -min kmin = max kmax
 
 // Base pixel of octave o at (y, x), coordinates already clamped to the plane.
 __device__ __forceinline__ double base_at(const Pyramid& P, int o, int y, int x) {

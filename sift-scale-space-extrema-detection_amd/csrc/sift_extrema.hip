@@ -78,15 +78,12 @@ __global__ __launch_bounds__(576) void k_extrema(const Pyramid P, const ExtremaL
   // Sliding 3-row window: per plane the 3-wide max/min of rows y-1, y, y+1;
   // the centre plane also keeps the 2-wide (x-1, x+1) max/min and the value.
   float mx[3][3], mn[3][3], emx[3], emn[3], cv[3];
-  auto load_row = [&](int yy, int slot) {
-    const long long row = (long long)yy * w;
-    const float* planes[3] = {Dm, Dc, Dq};
+  const float* planes[3] = {Dm, Dc, Dq};
+  auto derive = [&](const float (&v3)[3], const float (&e3)[3], int slot) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const float v = planes[q][row + xc];
-      float e = v;
-      if (is_edge) e = planes[q][row + xe];
-      const float vl = from_left(v, e), vr = from_right(v, e);
+      const float v = v3[q];
+      const float vl = from_left(v, e3[q]), vr = from_right(v, e3[q]);
       mx[q][slot] = max3f(vl, v, vr);
       mn[q][slot] = min3f(vl, v, vr);
       if (q == 1) {
@@ -96,10 +93,40 @@ __global__ __launch_bounds__(576) void k_extrema(const Pyramid P, const ExtremaL
       }
     }
   };
-  load_row(y0 - 1, 0);
-  load_row(y0, 1);
+  auto fetch = [&](int yy, float (&v3)[3], float (&e3)[3]) {
+    const long long row = (long long)min(yy, h - 1) * w;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      v3[q] = planes[q][row + xc];
+      e3[q] = is_edge ? planes[q][row + xe] : 0.0f;
+    }
+  };
+  {
+    float v3[3], e3[3];
+    fetch(y0 - 1, v3, e3);
+    derive(v3, e3, 0);
+    fetch(y0, v3, e3);
+    derive(v3, e3, 1);
+  }
+  // Rows are fetched kXG at a time so several loads per lane are in flight.
+  float pv[kXG][3], pe[kXG][3];
   for (int y = y0; y <= y1; ++y) {
-    load_row(y + 1, 2);
+    const int g = (y - y0) % kXG;
+    if (g == 0) {
+#pragma unroll
+      for (int k = 0; k < kXG; ++k) fetch(y + 1 + k, pv[k], pe[k]);
+    }
+    // select group slot g (static indices keep the arrays in registers)
+    float v3[3], e3[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) { v3[q] = pv[0][q]; e3[q] = pe[0][q]; }
+#pragma unroll
+    for (int k = 1; k < kXG; ++k)
+      if (g == k) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) { v3[q] = pv[k][q]; e3[q] = pe[k][q]; }
+      }
+    derive(v3, e3, 2);
     const float v = cv[1];
     const float nmax = max3f(max3f(mx[0][0], mx[0][1], mx[0][2]), max3f(mx[2][0], mx[2][1], mx[2][2]),
                              max3f(mx[1][0], mx[1][2], emx[1]));

@@ -18,11 +18,10 @@ struct GaussLaunch {
   float* dog;         // plane (o, 0) of the DoG pyramid
   double* next_seed;  // base of octave o+1 (nullptr for the last octave)
   int next_w;
-  int base_lds;       // stage the replicated-edge base region in LDS
-  int unfolded;       // octave 0 through the generic kernel (tests / A-B only)
 };
 
 constexpr int kXStrip = 64;  // rows per wave in the extrema scan
+constexpr int kXG = 4;       // rows fetched per group in the extrema scan
 
 struct ExtremaLaunch {
   int o;
@@ -69,8 +68,7 @@ struct RefineLaunch {
   unsigned* counters; // [3] n uncertain, [4] n singular
 };
 
-size_t gauss_lds_bytes(const Octave& oc, bool base_lds);
-size_t gauss_o0_lds_bytes(const Pyramid& P);
+size_t gauss_lds_bytes(const Octave& oc);
 hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t st);
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
 
