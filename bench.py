@@ -121,22 +121,14 @@ def main():
     torch.cuda.synchronize(dev)
     ctx = sift_amd.Context(dev)
 
-    kp_rec = sift_amd.KEYPOINT_DTYPE.itemsize
-    gather_state = {"buf": None, "cap": 0}
+    gather = None
+    if dist is not None:
+        from sift_amd.dist import KeypointGather
+        gather = KeypointGather("cuda:%d" % dev)
 
     def all_gather_keypoints(n):
-        cnt = torch.tensor([n], dtype=torch.int64, device="cuda:%d" % dev)
-        cnts = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(cnts, cnt)
-        m = int(max(int(c.item()) for c in cnts))
-        if gather_state["cap"] < max(m, 1):
-            cap = max(m, 1) + max(m, 1) // 4
-            gather_state["buf"] = torch.empty(cap * kp_rec, dtype=torch.uint8, device="cuda:%d" % dev)
-            gather_state["out"] = torch.empty(world * cap * kp_rec, dtype=torch.uint8, device="cuda:%d" % dev)
-            gather_state["cap"] = cap
-        ctx.copy_keypoints_device(gather_state["buf"].data_ptr(), gather_state["cap"])
-        dist.all_gather_into_tensor(gather_state["out"], gather_state["buf"])
-        return sum(int(c.item()) for c in cnts)
+        counts = gather(n, lambda buf, cap: ctx.copy_keypoints_device(buf.data_ptr(), cap))
+        return sum(counts)
 
     def step():
         n = ctx.detect_device(d_img.data_ptr(), W, H, params)

@@ -1,0 +1,79 @@
+"""Multi-GPU batch sharding: one process per GPU, RCCL keypoint all-gather.
+
+SURVEY.md §8(e): independent images shard across ranks with no exchange
+until the end; the only collective is the all-gather of the per-image
+keypoint lists (ragged: counts first, then records padded to the largest
+count).  torch.distributed with backend "nccl" is RCCL over xGMI on the GPU
+box; the same code runs on "gloo" with CPU tensors in the tests.
+
+Keypoint records are the 48-byte sift_keypoint (include/sift_hip.h), carried
+as raw uint8 rows so no reinterpretation happens on the wire.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import KEYPOINT_DTYPE
+
+REC = KEYPOINT_DTYPE.itemsize
+
+
+def shard_images(n_images, world, rank):
+    """Contiguous block of image indices for `rank` (weak scaling when
+    n_images = world * per_rank)."""
+    per, extra = divmod(n_images, world)
+    start = rank * per + min(rank, extra)
+    return list(range(start, start + per + (1 if rank < extra else 0)))
+
+
+class KeypointGather:
+    """Reusable all-gather of one ragged keypoint list per rank.
+
+    `fill(buf, cap)` writes this rank's records into `buf` (uint8 tensor of
+    cap*REC bytes, on `device`) and returns the count -- e.g. a device-to-
+    device copy from the HIP context (sift_copy_keypoints_device)."""
+
+    def __init__(self, device, group=None):
+        self.device = torch.device(device)
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.cap = 0
+        self.send = None
+        self.recv = None
+
+    def _ensure(self, cap):
+        if cap <= self.cap:
+            return
+        cap = max(cap, 1)
+        cap += cap // 4
+        self.send = torch.zeros(cap * REC, dtype=torch.uint8, device=self.device)
+        self.recv = torch.zeros(self.world * cap * REC, dtype=torch.uint8, device=self.device)
+        self.cap = cap
+
+    def __call__(self, n_local, fill):
+        cnt = torch.tensor([int(n_local)], dtype=torch.int64, device=self.device)
+        cnts = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(cnts, cnt, group=self.group)
+        counts = [int(c) for c in cnts.tolist()]
+        self._ensure(max(counts))
+        n = fill(self.send, self.cap)
+        assert n == n_local, (n, n_local)
+        dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        return counts
+
+    def gathered(self, counts):
+        """Host view: concatenation of every rank's records in rank order."""
+        raw = self.recv.view(self.world, self.cap * REC).cpu().numpy()
+        parts = [np.frombuffer(raw[r, :counts[r] * REC].tobytes(), dtype=KEYPOINT_DTYPE) for r in range(self.world)]
+        return np.concatenate(parts) if parts else np.zeros(0, dtype=KEYPOINT_DTYPE)
+
+
+def host_fill(records):
+    """fill() for host-side keypoint arrays (tests / CPU ranks)."""
+    raw = np.ascontiguousarray(records, dtype=KEYPOINT_DTYPE).view(np.uint8)
+
+    def fill(buf, cap):
+        if raw.size:
+            buf[:raw.size].copy_(torch.from_numpy(raw.copy()).to(buf.device))
+        return records.shape[0]
+    return fill
