@@ -272,7 +272,7 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
   if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");
   // LDS feasibility of the Gaussian kernel (strip of min(h, 32+2R) fp64 rows).
   for (int o = 0; o < O; ++o)
-    if (gauss_lds_bytes(P.oct[o]) > 160 * 1024)
+    if (gauss_lds_bytes(P, o) > 160 * 1024)
       return set_err(ctx, SIFT_E_UNSUPPORTED, "blur radius too large for one LDS strip");
   if (need_weights) {
     if (ctx->wts.ensure(w.size() * sizeof(double)) != hipSuccess)

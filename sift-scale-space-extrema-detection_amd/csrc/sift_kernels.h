@@ -68,7 +68,7 @@ struct RefineLaunch {
   unsigned* counters; // [3] n uncertain, [4] n singular
 };
 
-size_t gauss_lds_bytes(const Octave& oc);
+size_t gauss_lds_bytes(const Pyramid& P, int o);
 hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t st);
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
 
