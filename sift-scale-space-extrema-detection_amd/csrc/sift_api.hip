@@ -461,6 +461,14 @@ int sift_load_scale_space(sift_ctx* ctx, const float* planes, int width, int hei
 // Extrema: scan -> sort by (octave, scale, y, x) -> exact tie resolution ->
 // ordered compaction.  Leaves ctx->cand_key / cand_val / n_cand.
 // ---------------------------------------------------------------------------
+// Nearest fp32 at or below (dir < 0) / at or above (dir > 0) a double.
+static float round_toward(double v, int dir) {
+  float f = (float)v;
+  if (dir < 0 && (double)f > v) f = std::nextafter(f, -INFINITY);
+  if (dir > 0 && (double)f < v) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
 static int run_extrema(sift_ctx* ctx) {
   Pyramid& P = ctx->P;
   const bool exact_planes = ctx->dog_source == kForeign;
@@ -469,12 +477,15 @@ static int run_extrema(sift_ctx* ctx) {
   std::vector<long long> word_off(P.O), row_off(P.O);
   long long words = 0, rows = 0;
   for (int o = 0; o < P.O; ++o) {
-    const int nw = (P.oct[o].w + 63) / 64;
+    const int nw = extrema_words_per_row(P.oct[o].w);
     word_off[o] = words;
     row_off[o] = rows;
     words += (long long)P.S * P.oct[o].h * nw;
     rows += (long long)P.S * P.oct[o].h;
   }
+  // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
+  // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
+  const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
   HIPCHK(ctx->bitmap.ensure((size_t)words * sizeof(unsigned long long)));
   HIPCHK(ctx->rowcount.ensure((size_t)(rows + 1) * sizeof(unsigned)));
   HIPCHK(ctx->rowoff.ensure((size_t)(rows + 1) * sizeof(unsigned)));
@@ -485,18 +496,20 @@ static int run_extrema(sift_ctx* ctx) {
     HIPCHK(ctx->amb_keys.ensure((size_t)amb_cap * sizeof(unsigned)));
     HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), ctx->stream));
+    ExtremaLaunch L{};
+    L.exact_planes = exact_planes;
+    L.c_lo = exact_planes ? t_up : t_dn;
+    L.c_hi = exact_planes ? t_up : std::nextafter(t_up, INFINITY);
+    L.bitmap = ctx->bitmap.as<unsigned long long>();
+    L.rowcount = ctx->rowcount.as<unsigned>();
     for (int o = 0; o < P.O; ++o) {
-      ExtremaLaunch L{};
-      L.o = o;
-      L.exact_planes = exact_planes;
-      L.bitmap = ctx->bitmap.as<unsigned long long>() + word_off[o];
-      L.nw = (P.oct[o].w + 63) / 64;
-      L.rowcount = ctx->rowcount.as<unsigned>() + row_off[o];
-      L.amb_keys = ctx->amb_keys.as<unsigned>();
-      L.counters = cnt;
-      L.amb_cap = amb_cap;
-      HIPCHK(launch_extrema(P, L, ctx->stream));
+      L.word_off[o] = word_off[o];
+      L.row_off[o] = (int)row_off[o];
     }
+    L.amb_keys = ctx->amb_keys.as<unsigned>();
+    L.counters = cnt;
+    L.amb_cap = amb_cap;
+    HIPCHK(launch_extrema(P, L, ctx->stream));
     size_t tb = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
                                             (int)(rows + 1), ctx->stream));
@@ -520,7 +533,7 @@ static int run_extrema(sift_ctx* ctx) {
     EmitLaunch E{};
     E.o = o;
     E.bitmap = ctx->bitmap.as<unsigned long long>() + word_off[o];
-    E.nw = (P.oct[o].w + 63) / 64;
+    E.nw = extrema_words_per_row(P.oct[o].w);
     E.rowcount = ctx->rowcount.as<unsigned>() + row_off[o];
     E.rowoff = ctx->rowoff.as<unsigned>();
     E.row_base = (int)row_off[o];

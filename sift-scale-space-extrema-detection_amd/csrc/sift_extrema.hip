@@ -7,12 +7,14 @@
 // it is a low-contrast extremum.  Output order is the reference's: octave,
 // scale, then raster (y, x).
 //
-// k_extrema: one block per (64-column word, strip of kXStrip rows), one wave
-// per DoG scale, sliding a 3-row window down the strip.  Each lane loads its
-// column of the three DoG planes, takes x-1 / x+1 from its neighbours with
-// DPP wave shifts (word edges from one extra load), reduces the 26
-// neighbours with max3/min3, and ballots the candidate mask of the 64 pixels
-// straight into a bitmap word [s][y][x/64] plus a per-row popcount.  k_emit
+// k_extrema: one wave per (62-column word, strip of kXRows rows, group of up
+// to 5 scales), sliding a 3-row window down the strip over all the group's
+// DoG planes.  Lanes 1..62 are output columns, lanes 0 and 63 their halo, so
+// x-1 / x+1 come from DPP wave shifts without extra loads.  Each plane row is
+// reduced once (3-wide max/min) and shared by the scales above and below it;
+// the 26-neighbour decision is 6 compares per scale, the rest is lane-mask
+// logic whose result is the bitmap word [s][y][word] directly, plus a per-row
+// popcount.  k_emit
 // expands the bitmap in order after an exclusive scan of the row counts --
 // the candidate list comes out sorted without a sort.
 //
@@ -40,140 +42,201 @@ __device__ __forceinline__ unsigned wave_append(bool pred, unsigned* counter) {
   return base + lane_prefix(mask);
 }
 
-// Value of lane-1 (lane 0 takes `edge`) / lane+1 (lane 63 takes `edge`).
-__device__ __forceinline__ float from_left(float v, float edge) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x138, 0xF, 0xF, false));
+// Lane l-1 / lane l+1 of a wave (DPP wave shifts; lanes 0 / 63 get 0, they
+// are halo lanes whose results are never used).
+__device__ __forceinline__ float from_left(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true));
 }
-__device__ __forceinline__ float from_right(float v, float edge) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), 0x130, 0xF, 0xF, false));
+__device__ __forceinline__ float from_right(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
 }
 
-__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(a, fmaxf(b, c)); }
-__device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(a, fminf(b, c)); }
+__device__ __forceinline__ float max3f(float a, float b, float c) { return __builtin_fmaxf(a, __builtin_fmaxf(b, c)); }
+__device__ __forceinline__ float min3f(float a, float b, float c) { return __builtin_fminf(a, __builtin_fminf(b, c)); }
 
-// One block per (64-column word, strip of kXStrip rows); wave s-1 of the
-// block scans DoG scale s.  The S waves of a block read overlapping planes
-// at the same rows, so each plane streams from HBM about once (L1/L2 reuse).
-__global__ __launch_bounds__(576) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
-  const Octave& oc = P.oct[L.o];
-  const int h = oc.h, w = oc.w;
-  const int lane = threadIdx.x & 63;
-  const int s = 1 + (threadIdx.x >> 6);
-  const int xw = blockIdx.x;
-  const int y0 = 1 + blockIdx.y * kXStrip;
-  const int y1 = min(h - 2, y0 + kXStrip - 1);
-  const long long plane = (long long)h * w;
-  const float* __restrict__ D = P.dog + oc.dog_off;
-  const float* __restrict__ Dm = D + (s - 1) * plane;
-  const float* __restrict__ Dc = D + s * plane;
-  const float* __restrict__ Dq = D + (s + 1) * plane;
-  const double T = P.pix_thr;
-  const int x = xw * 64 + lane;
-  const int xc = min(x, w - 1);
-  const bool is_edge = lane == 0 || lane == 63;
-  const int xe = clampi(lane == 0 ? x - 1 : x + 1, 0, w - 1);
-  const bool col_ok = x >= 1 && x <= w - 2;
-  unsigned low = 0;
+// Per-wave state of the 3-row window over NP consecutive DoG planes (the
+// centre planes 1..NP-2 are scales, 0 and NP-1 their outer neighbours).
+// Slot k holds the row whose offset from the group's first centre row is
+// k mod 3; all indices are compile-time constants, so nothing rotates.
+template <int NP>
+struct XWin {
+  float hx[3][NP], hn[3][NP];  // 3-wide max / min of a row
+  float ex[3][NP], en[3][NP];  // 2-wide (x-1, x+1) max / min (centre planes)
+  float cv[3][NP];             // the value (centre planes)
+  float raw[3][NP];            // loaded, not yet derived rows
+};
 
-  // Sliding 3-row window: per plane the 3-wide max/min of rows y-1, y, y+1;
-  // the centre plane also keeps the 2-wide (x-1, x+1) max/min and the value.
-  float mx[3][3], mn[3][3], emx[3], emn[3], cv[3];
-  const float* planes[3] = {Dm, Dc, Dq};
-  auto derive = [&](const float (&v3)[3], const float (&e3)[3], int slot) {
+template <int NP>
+struct XUnit {
+  const float* base;   // DoG plane of the group's first plane, row 0
+  long long plane;
+  __amdgpu_buffer_rsrc_t rsrc;  // the group's DoG planes
+  unsigned plane_bytes;  // < 4 GiB per group (launch_extrema checks)
+  int w, h, y1;
+  unsigned xoff;       // lane byte offset of its (clamped) column
+  unsigned long long colmask;  // lanes with an interior output column
+  int lane, xw, nw, s_first, o;
+  unsigned key_base;   // key of (s_first, 0, 0)
+  unsigned long long* bitmap;  // (s_first, row 0, word 0) of this octave
+  unsigned* rowcount;          // (s_first, row 0) of this octave
+  unsigned low;
+};
+
+template <int NP>
+__device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int row) {
+  // buffer loads: lane byte offset in a VGPR, row + plane offset in an SGPR
+  const unsigned rofs = (unsigned)row * (unsigned)U.w * 4u;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const float v = v3[q];
-      const float vl = from_left(v, e3[q]), vr = from_right(v, e3[q]);
-      mx[q][slot] = max3f(vl, v, vr);
-      mn[q][slot] = min3f(vl, v, vr);
-      if (q == 1) {
-        emx[slot] = fmaxf(vl, vr);
-        emn[slot] = fminf(vl, vr);
-        cv[slot] = v;
-      }
-    }
-  };
-  auto fetch = [&](int yy, float (&v3)[3], float (&e3)[3]) {
-    const long long row = (long long)min(yy, h - 1) * w;
+  for (int q = 0; q < NP; ++q)
+    dst[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           U.rsrc, (int)U.xoff, (int)(rofs + (unsigned)q * U.plane_bytes), 0));
+}
+
+template <int NP, int K>
+__device__ __forceinline__ void x_derive(XWin<NP>& Wn, const float (&src)[NP]) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      v3[q] = planes[q][row + xc];
-      e3[q] = is_edge ? planes[q][row + xe] : 0.0f;
+  for (int q = 0; q < NP; ++q) {
+    const float v = src[q];
+    const float l = from_left(v), r = from_right(v);
+    const float m2 = __builtin_fmaxf(l, r), n2 = __builtin_fminf(l, r);
+    Wn.hx[K][q] = __builtin_fmaxf(m2, v);
+    Wn.hn[K][q] = __builtin_fminf(n2, v);
+    if (q >= 1 && q <= NP - 2) {
+      Wn.ex[K][q] = m2;
+      Wn.en[K][q] = n2;
+      Wn.cv[K][q] = v;
     }
-  };
+  }
+}
+
+// Centre row y (slots A = y-1, B = y, C = y+1): decide every scale of the group.
+template <int NP, int A, int B, int C>
+__device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const ExtremaLaunch& L, int y) {
+  float vx[NP], vn[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    vx[q] = max3f(Wn.hx[A][q], Wn.hx[B][q], Wn.hx[C][q]);
+    vn[q] = min3f(Wn.hn[A][q], Wn.hn[B][q], Wn.hn[C][q]);
+  }
+  unsigned wlo = 0, whi = 0, wcnt = 0;
+#pragma unroll
+  for (int q = 1; q <= NP - 2; ++q) {
+    const float v = Wn.cv[B][q];
+    const float nmax = max3f(vx[q - 1], vx[q + 1], max3f(Wn.hx[A][q], Wn.hx[C][q], Wn.ex[B][q]));
+    const float nmin = min3f(vn[q - 1], vn[q + 1], min3f(Wn.hn[A][q], Wn.hn[C][q], Wn.en[B][q]));
+    const float av = __builtin_fabsf(v);
+    // Lane masks (SALU from here on).
+    const unsigned long long ge = __ballot(v >= nmax), le = __ballot(v <= nmin);
+    const unsigned long long gt = __ballot(v > nmax), lt = __ballot(v < nmin);
+    const unsigned long long lo = __ballot(av < L.c_lo), hi = __ballot(av >= L.c_hi);
+    const unsigned long long certain = (gt | lt) & U.colmask;
+    unsigned long long ext, tie;
+    if (L.exact_planes) { ext = certain; tie = 0ull; }
+    else { ext = (ge | le) & U.colmask; tie = ext & ~certain; }
+    const unsigned long long count_low = ext & lo & ~tie;
+    const unsigned long long bit = ext & ~count_low;
+    const unsigned long long amb = bit & (tie | ~hi);
+    U.low += (unsigned)__popcll(count_low);
+    const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
+    if (U.lane == q - 1) {
+      wlo = (unsigned)word;
+      whi = (unsigned)(word >> 32);
+      wcnt = (unsigned)__popcll(word);
+    }
+    if (amb) {  // rare: ties / contrast within fp32 rounding of the threshold
+      const bool mine = (amb >> U.lane) & 1ull;
+      const unsigned slot = wave_append(mine, &L.counters[0]);
+      if (mine && slot < L.amb_cap)
+        L.amb_keys[slot] = U.key_base + (unsigned)(q - 1) * (unsigned)U.plane + (unsigned)y * (unsigned)U.w +
+                           (unsigned)(U.xw * kXW - 1 + U.lane);
+    }
+  }
+  if (U.lane < NP - 2) {
+    const long long r = (long long)U.lane * U.h + y;
+    U.bitmap[r * U.nw + U.xw] = ((unsigned long long)whi << 32) | wlo;
+    if (wcnt) atomicAdd(&U.rowcount[r], wcnt);
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int o, int s_first, int xw,
+                                       int y0, int y1) {
+  const Octave& oc = P.oct[o];
+  XUnit<NP> U;
+  U.plane = (long long)oc.h * oc.w;
+  U.w = oc.w;
+  U.h = oc.h;
+  U.y1 = y1;
+  U.lane = threadIdx.x & 63;
+  U.xw = xw;
+  U.nw = L.nw[o];
+  U.s_first = s_first;
+  U.o = o;
+  const int x = xw * kXW - 1 + U.lane;
+  U.xoff = 4u * (unsigned)clampi(x, 0, oc.w - 1);
+  U.plane_bytes = (unsigned)(4 * U.plane);
+  U.colmask = __ballot(U.lane >= 1 && U.lane <= kXW && x >= 1 && x <= oc.w - 2);
+  U.base = P.dog + oc.dog_off + (long long)(s_first - 1) * U.plane;
+  U.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(U.base), 0, -1, 0x00020000);
+  U.key_base = oc.key_off + (unsigned)(s_first - 1) * (unsigned)U.plane;
+  U.bitmap = L.bitmap + L.word_off[o] + (long long)(s_first - 1) * oc.h * U.nw;
+  U.rowcount = L.rowcount + L.row_off[o] + (s_first - 1) * oc.h;
+  U.low = 0;
+
+  XWin<NP> Wn;
   {
-    float v3[3], e3[3];
-    fetch(y0 - 1, v3, e3);
-    derive(v3, e3, 0);
-    fetch(y0, v3, e3);
-    derive(v3, e3, 1);
+    float r_m1[NP], r_0[NP];
+    x_load(U, r_m1, y0 - 1);
+    x_load(U, r_0, y0);
+    x_load(U, Wn.raw[1], y0 + 1);
+    x_load(U, Wn.raw[2], min(y0 + 2, y1 + 1));
+    x_load(U, Wn.raw[0], min(y0 + 3, y1 + 1));
+    x_derive<NP, 2>(Wn, r_m1);
+    x_derive<NP, 0>(Wn, r_0);
   }
-  // Rows are fetched kXG at a time so several loads per lane are in flight.
-  float pv[kXG][3], pe[kXG][3];
-  for (int y = y0; y <= y1; ++y) {
-    const int g = (y - y0) % kXG;
-    if (g == 0) {
-#pragma unroll
-      for (int k = 0; k < kXG; ++k) fetch(y + 1 + k, pv[k], pe[k]);
-    }
-    // select group slot g (static indices keep the arrays in registers)
-    float v3[3], e3[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) { v3[q] = pv[0][q]; e3[q] = pe[0][q]; }
-#pragma unroll
-    for (int k = 1; k < kXG; ++k)
-      if (g == k) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) { v3[q] = pv[k][q]; e3[q] = pe[k][q]; }
-      }
-    derive(v3, e3, 2);
-    const float v = cv[1];
-    const float nmax = max3f(max3f(mx[0][0], mx[0][1], mx[0][2]), max3f(mx[2][0], mx[2][1], mx[2][2]),
-                             max3f(mx[1][0], mx[1][2], emx[1]));
-    const float nmin = min3f(min3f(mn[0][0], mn[0][1], mn[0][2]), min3f(mn[2][0], mn[2][1], mn[2][2]),
-                             min3f(mn[1][0], mn[1][2], emn[1]));
-    const bool possible = v >= nmax || v <= nmin;  // no neighbour strictly beyond v
-    const bool certain = v > nmax || v < nmin;     // strict in fp32 => strict in fp64
-    bool ext, tie;
-    if (L.exact_planes) { ext = certain; tie = false; }
-    else { ext = possible; tie = !certain; }
-    ext = ext && col_ok;
-    const double av = fabs((double)v);
-    bool low_certain, contrast_amb = false;
-    if (L.exact_planes) {
-      low_certain = av < T;
-    } else {
-      const double e = av * 0x1p-24 + 1e-300;  // |v - v_fp64| <= ulp/2 <= |v| 2^-24
-      low_certain = av + e < T;
-      contrast_amb = !low_certain && av - e < T;
-    }
-    const bool count_low = ext && low_certain && !tie;
-    const bool bit = ext && !count_low;
-    low += count_low ? 1u : 0u;
-    const unsigned long long word = __ballot(bit);
-    if (lane == 0) {
-      L.bitmap[((long long)(s - 1) * h + y) * L.nw + xw] = word;
-      if (word) atomicAdd(&L.rowcount[(s - 1) * h + y], (unsigned)__popcll(word));
-    }
-    const bool amb = bit && (tie || contrast_amb);
-    if (__ballot(amb)) {  // rare
-      const unsigned slot = wave_append(amb, &L.counters[0]);
-      if (amb && slot < L.amb_cap)
-        L.amb_keys[slot] = oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w + (unsigned)x;
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      mx[q][0] = mx[q][1]; mx[q][1] = mx[q][2];
-      mn[q][0] = mn[q][1]; mn[q][1] = mn[q][2];
-    }
-    emx[0] = emx[1]; emx[1] = emx[2];
-    emn[0] = emn[1]; emn[1] = emn[2];
-    cv[0] = cv[1]; cv[1] = cv[2];
+  // Each row's loads are issued three rows before it is derived (rows past
+  // the strip re-read row y1+1 from L2 instead of branching).
+  for (int y = y0; y <= y1; y += 3) {
+    x_derive<NP, 1>(Wn, Wn.raw[1]);
+    x_load(U, Wn.raw[1], min(y + 4, y1 + 1));
+    x_centre<NP, 2, 0, 1>(Wn, U, L, y);
+    if (y + 1 > y1) break;
+    x_derive<NP, 2>(Wn, Wn.raw[2]);
+    x_load(U, Wn.raw[2], min(y + 5, y1 + 1));
+    x_centre<NP, 0, 1, 2>(Wn, U, L, y + 1);
+    if (y + 2 > y1) break;
+    x_derive<NP, 0>(Wn, Wn.raw[0]);
+    x_load(U, Wn.raw[0], min(y + 6, y1 + 1));
+    x_centre<NP, 1, 2, 0>(Wn, U, L, y + 2);
   }
-  // wave sum of the low-contrast count, one atomic per wave
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) low += __shfl_xor(low, off);
-  if (lane == 0 && low) atomicAdd(&L.counters[1], low);
+  if (U.lane == 0 && U.low) atomicAdd(&L.counters[1], U.low);
+}
+
+// One wave per unit (octave, strip of kXRows rows, 62-column word, scale
+// group): all DoG planes of the group stream through once, each plane's row
+// is reduced once (3-wide max/min with DPP shifts) and shared by the scales
+// above and below it; the decisions are SALU lane-mask logic.
+__global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
+  const int u = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (u >= L.unit_off[L.n_oct]) return;
+  int o = 0;
+  while (o + 1 < L.n_oct && u >= L.unit_off[o + 1]) ++o;
+  int loc = u - L.unit_off[o];
+  const int g = loc % L.ng;
+  loc /= L.ng;
+  const int nw = L.nw[o];
+  const int xw = loc % nw, strip = loc / nw;
+  const int y0 = 1 + strip * kXRows, y1 = min(P.oct[o].h - 2, y0 + kXRows - 1);
+  const int per = P.S / L.ng, rem = P.S % L.ng;
+  const int s_first = 1 + g * per + min(g, rem);
+  const int cnt = per + (g < rem ? 1 : 0);
+  switch (cnt) {
+    case 1: x_scan<3>(P, L, o, s_first, xw, y0, y1); break;
+    case 2: x_scan<4>(P, L, o, s_first, xw, y0, y1); break;
+    case 3: x_scan<5>(P, L, o, s_first, xw, y0, y1); break;
+    case 4: x_scan<6>(P, L, o, s_first, xw, y0, y1); break;
+    default: x_scan<7>(P, L, o, s_first, xw, y0, y1); break;
+  }
 }
 
 // One wave per (scale, row) of one octave: expand the row's bitmap words in
@@ -208,7 +271,7 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
     while (word) {
       const int b = __ffsll((long long)word) - 1;
       word &= word - 1;
-      const int x = xw * 64 + b;
+      const int x = xw * kXW + b;
       E.keys[pos] = kbase + (unsigned)x;
       E.value[pos] = (double)Dc[x];
       E.keep[pos] = 1u;
@@ -253,11 +316,22 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
   }
 }
 
-hipError_t launch_extrema(const Pyramid& P, const ExtremaLaunch& L, hipStream_t st) {
-  const Octave& oc = P.oct[L.o];
-  if (oc.h < 3 || oc.w < 3 || P.S < 1) return hipSuccess;  // no interior pixels
-  const int strips = (oc.h - 2 + kXStrip - 1) / kXStrip;
-  hipLaunchKernelGGL(k_extrema, dim3(L.nw, strips), dim3(64 * P.S), 0, st, P, L);
+hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st) {
+  L.n_oct = P.O;
+  L.ng = (P.S + kXMaxGroup - 1) / kXMaxGroup;
+  int units = 0;
+  for (int o = 0; o < P.O; ++o) {
+    const Octave& oc = P.oct[o];
+    L.unit_off[o] = units;
+    L.nw[o] = extrema_words_per_row(oc.w);
+    if (oc.h >= 3 && oc.w >= 3 && P.S >= 1) units += L.ng * L.nw[o] * ((oc.h - 2 + kXRows - 1) / kXRows);
+  }
+  L.unit_off[P.O] = units;
+  if (units == 0) return hipSuccess;
+  // 32-bit buffer offsets cover one scale group's planes
+  const int np = std::min(P.S, kXMaxGroup) + 2;
+  if (4.0 * np * (double)P.oct[0].h * P.oct[0].w >= 4294967296.0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_extrema, dim3((units + 3) / 4), dim3(256), 0, st, P, L);
   return hipGetLastError();
 }
 

@@ -20,15 +20,23 @@ struct GaussLaunch {
   int next_w;
 };
 
-constexpr int kXStrip = 64;  // rows per wave in the extrema scan
-constexpr int kXG = 4;       // rows fetched per group in the extrema scan
+constexpr int kXW = 62;      // output columns per extrema wave (lanes 1..62; lanes 0, 63 are halo)
+constexpr int kXRows = 30;   // centre rows per extrema wave (multiple of 3)
+constexpr int kXMaxGroup = 5;// scales per extrema wave (S > 5 splits the scales into groups)
 
+// One launch scans every octave: unit u (one wave) = (octave, strip of kXRows
+// rows, 62-column word, scale group).
 struct ExtremaLaunch {
-  int o;
+  int n_oct;
   int exact_planes;              // DoG planes are the data itself (caller-supplied): no fp32 ties
-  unsigned long long* bitmap;    // this octave's candidate bitmap [S][h][nw]
-  int nw;                        // 64-pixel words per row
-  unsigned* rowcount;            // this octave's candidates per (scale, row) [S][h]
+  int ng;                        // scale groups per (strip, word)
+  float c_lo, c_hi;              // |v| < c_lo: certainly low contrast; |v| >= c_hi: certainly not
+  int unit_off[kMaxOctaves + 1]; // first unit of each octave
+  int nw[kMaxOctaves];           // words per row
+  long long word_off[kMaxOctaves];  // first bitmap word of each octave ([S][h][nw])
+  int row_off[kMaxOctaves];      // first row count of each octave ([S][h])
+  unsigned long long* bitmap;
+  unsigned* rowcount;
   unsigned* amb_keys;            // keys needing an exact fp64 decision (unordered)
   unsigned* counters;            // [0] ambiguous, [1] low-contrast, [2] dropped by exact pass
   unsigned amb_cap;
@@ -72,7 +80,10 @@ size_t gauss_lds_bytes(const Pyramid& P, int o);
 hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t st);
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
 
-hipError_t launch_extrema(const Pyramid& P, const ExtremaLaunch& L, hipStream_t st);
+// Fills the unit table of L (octave geometry) and launches the scan; returns
+// the launch error.  L.bitmap words per octave: S * h * nw.
+hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st);
+inline int extrema_words_per_row(int w) { return (w + kXW - 1) / kXW; }
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st);
 // One wave per ambiguous candidate: fp64 pointwise recompute of the 3x3x3 DoG patch.
 hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, unsigned n_amb, hipStream_t st);
