@@ -5,6 +5,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -63,6 +64,10 @@ struct sift_ctx {
   bool have_cand = false;
   size_t n_cand = 0, n_low = 0, n_kp = 0, n_sing = 0, n_exact = 0;
   size_t n_slots = 0;       // candidate slots (n_cand + entries dropped by the exact pass)
+  unsigned cand_cap = 0;    // capacity of the candidate slot arrays (extrema path)
+  unsigned amb_cap = 0;     // capacity of the ambiguous-key list
+  int slot_cap = 0;         // slots the refinement runs over
+  bool ext_pending = false; // extrema launched, counts not yet read back
   bool has_keep = false;    // slots carry keep flags
   // device memory
   DBuf img, seeds, gauss, dog, wts;
@@ -469,7 +474,15 @@ static float round_toward(double v, int dir) {
   return f;
 }
 
-static int run_extrema(sift_ctx* ctx) {
+// Counter slots (ctx->counters): [0] ambiguous keys, [1] low-contrast
+// extrema, [2] slots dropped by the exact pass, [3] uncertain refinements,
+// [4] singular Hessians, [12] candidate slots, [13] keypoints, [16..] debug.
+enum { kCntAmb = 0, kCntLow = 1, kCntDrop = 2, kCntUnc = 3, kCntSing = 4, kCntN = 12, kCntKp = 13 };
+constexpr int kRetry = 1;  // internal: a capacity overflowed, grow and run again
+
+// Launches the extrema stage without waiting: bitmap scan, ordered emission
+// into cand_cap slots, exact tie resolution.  Counts stay on the device.
+static int launch_extrema_stage(sift_ctx* ctx) {
   Pyramid& P = ctx->P;
   const bool exact_planes = ctx->dog_source == kForeign;
   unsigned* cnt = ctx->counters.as<unsigned>();
@@ -483,52 +496,48 @@ static int run_extrema(sift_ctx* ctx) {
     words += (long long)P.S * P.oct[o].h * nw;
     rows += (long long)P.S * P.oct[o].h;
   }
-  // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
-  // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
-  const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
+  {  // capacities: an estimate for this geometry, grown on overflow (settle_extrema)
+    const long long est = std::min<long long>(std::max<long long>((long long)P.S * total_plane_px(ctx) / 192, 65536),
+                                              0x7fffffffLL);
+    ctx->cand_cap = std::max(ctx->cand_cap, (unsigned)est);
+    ctx->amb_cap = std::max(ctx->amb_cap, 4096 + (unsigned)est / 16);
+  }
   HIPCHK(ctx->bitmap.ensure((size_t)words * sizeof(unsigned long long)));
   HIPCHK(ctx->rowcount.ensure((size_t)(rows + 1) * sizeof(unsigned)));
   HIPCHK(ctx->rowoff.ensure((size_t)(rows + 1) * sizeof(unsigned)));
-  unsigned amb_cap = (unsigned)std::max<size_t>(4096, ctx->amb_keys.bytes / sizeof(unsigned));
+  HIPCHK(ctx->amb_keys.ensure((size_t)ctx->amb_cap * sizeof(unsigned)));
+  HIPCHK(ctx->cand_key.ensure((size_t)ctx->cand_cap * sizeof(unsigned)));
+  HIPCHK(ctx->cand_val.ensure((size_t)ctx->cand_cap * sizeof(double)));
+  HIPCHK(ctx->cand_keep.ensure((size_t)ctx->cand_cap * sizeof(unsigned)));
+  // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
+  // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
+  const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  unsigned n_amb = 0;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    HIPCHK(ctx->amb_keys.ensure((size_t)amb_cap * sizeof(unsigned)));
-    HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), ctx->stream));
-    ExtremaLaunch L{};
-    L.exact_planes = exact_planes;
-    L.c_lo = exact_planes ? t_up : t_dn;
-    L.c_hi = exact_planes ? t_up : std::nextafter(t_up, INFINITY);
-    L.bitmap = ctx->bitmap.as<unsigned long long>();
-    L.rowcount = ctx->rowcount.as<unsigned>();
-    for (int o = 0; o < P.O; ++o) {
-      L.word_off[o] = word_off[o];
-      L.row_off[o] = (int)row_off[o];
-    }
-    L.amb_keys = ctx->amb_keys.as<unsigned>();
-    L.counters = cnt;
-    L.amb_cap = amb_cap;
-    HIPCHK(launch_extrema(P, L, ctx->stream));
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
-                                            (int)(rows + 1), ctx->stream));
-    HIPCHK(ctx->temp.ensure(tb));
-    tb = ctx->temp.bytes;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
-                                            (int)(rows + 1), ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->h_counters + 8, ctx->rowoff.as<unsigned>() + rows, sizeof(unsigned),
-                          hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    n_amb = ctx->h_counters[0];
-    if (n_amb <= amb_cap) break;
-    amb_cap = n_amb + n_amb / 4 + 1024;
+  HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), ctx->stream));
+  HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), ctx->stream));
+  ExtremaLaunch L{};
+  L.exact_planes = exact_planes;
+  L.c_lo = exact_planes ? t_up : t_dn;
+  L.c_hi = exact_planes ? t_up : std::nextafter(t_up, INFINITY);
+  L.bitmap = ctx->bitmap.as<unsigned long long>();
+  L.rowcount = ctx->rowcount.as<unsigned>();
+  for (int o = 0; o < P.O; ++o) {
+    L.word_off[o] = word_off[o];
+    L.row_off[o] = (int)row_off[o];
   }
-  const unsigned n = ctx->h_counters[8];
-  HIPCHK(ctx->cand_key.ensure((size_t)std::max(n, 1u) * sizeof(unsigned)));
-  HIPCHK(ctx->cand_val.ensure((size_t)std::max(n, 1u) * sizeof(double)));
-  HIPCHK(ctx->cand_keep.ensure((size_t)std::max(n, 1u) * sizeof(unsigned)));
+  L.amb_keys = ctx->amb_keys.as<unsigned>();
+  L.counters = cnt;
+  L.amb_cap = ctx->amb_cap;
+  HIPCHK(launch_extrema(P, L, ctx->stream));
+  size_t tb = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
+                                          (int)(rows + 1), ctx->stream));
+  HIPCHK(ctx->temp.ensure(tb));
+  tb = ctx->temp.bytes;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
+                                          (int)(rows + 1), ctx->stream));
+  HIPCHK(hipMemcpyAsync(cnt + kCntN, ctx->rowoff.as<unsigned>() + rows, sizeof(unsigned), hipMemcpyDeviceToDevice,
+                        ctx->stream));
   for (int o = 0; o < P.O; ++o) {
     EmitLaunch E{};
     E.o = o;
@@ -540,50 +549,83 @@ static int run_extrema(sift_ctx* ctx) {
     E.keys = ctx->cand_key.as<unsigned>();
     E.value = ctx->cand_val.as<double>();
     E.keep = ctx->cand_keep.as<unsigned>();
+    E.cap = ctx->cand_cap;
     HIPCHK(launch_emit(P, E, ctx->stream));
   }
-  ctx->n_exact = n_amb;
-  if (n_amb) {
-    ExactLaunch X{};
-    X.amb_keys = ctx->amb_keys.as<unsigned>();
-    X.keys = ctx->cand_key.as<unsigned>();
-    X.n = n;
-    X.keep = ctx->cand_keep.as<unsigned>();
-    X.value = ctx->cand_val.as<double>();
-    X.counters = cnt;
-    HIPCHK(launch_exact_extrema(P, X, n_amb, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-  }
-  ctx->n_low = ctx->h_counters[1];
-  ctx->n_slots = n;
-  ctx->n_cand = n - (n_amb ? ctx->h_counters[2] : 0);
-  ctx->has_keep = true;
+  ExactLaunch X{};
+  X.amb_keys = ctx->amb_keys.as<unsigned>();
+  X.amb_cap = ctx->amb_cap;
+  X.keys = ctx->cand_key.as<unsigned>();
+  X.n = cnt + kCntN;
+  X.cap = ctx->cand_cap;
+  X.keep = ctx->cand_keep.as<unsigned>();
+  X.value = ctx->cand_val.as<double>();
+  X.counters = cnt;
+  HIPCHK(launch_exact_extrema(P, X, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
+  ctx->slot_cap = (int)ctx->cand_cap;
+  ctx->has_keep = true;
+  ctx->ext_pending = true;
+  return SIFT_OK;
+}
+
+// Reads the extrema counts (ctx->h_counters must hold the device counters):
+// kRetry after growing the capacities when one overflowed.
+static int settle_extrema(sift_ctx* ctx) {
+  const unsigned* h = ctx->h_counters;
+  ctx->ext_pending = false;
+  const unsigned n = h[kCntN], n_amb = h[kCntAmb];
+  if (n > ctx->cand_cap || n_amb > ctx->amb_cap) {
+    if (n > ctx->cand_cap) ctx->cand_cap = n + n / 4 + 1024;
+    if (n_amb > ctx->amb_cap) ctx->amb_cap = n_amb + n_amb / 4 + 1024;
+    return kRetry;
+  }
+  ctx->n_exact = n_amb;
+  ctx->n_low = h[kCntLow];
+  ctx->n_slots = n;
+  ctx->n_cand = n - h[kCntDrop];
   ctx->have_cand = true;
   return SIFT_OK;
 }
 
+static int run_extrema(sift_ctx* ctx) {
+  for (;;) {
+    int rc = launch_extrema_stage(ctx);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(ctx->h_counters, ctx->counters.p, 16 * sizeof(unsigned), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    rc = settle_extrema(ctx);
+    if (rc != kRetry) return rc;
+  }
+}
+
+// Refinement over ctx->slot_cap slots, *counters[12] of them live, without
+// a host round trip; one synchronisation at the end reads every count back.
+// Returns kRetry when the extrema stage it follows overflowed.
 static int run_refine(sift_ctx* ctx) {
   Pyramid& P = ctx->P;
-  const int n = (int)ctx->n_slots;
+  const int cap = ctx->slot_cap;
   unsigned* cnt = ctx->counters.as<unsigned>();
   HIPCHK(hipEventRecord(ctx->ev[5], ctx->stream));
-  HIPCHK(ctx->status.ensure((size_t)std::max(n, 1) * sizeof(int)));
-  HIPCHK(ctx->kp_tmp.ensure((size_t)std::max(n, 1) * sizeof(Keypoint)));
-  HIPCHK(ctx->kp.ensure((size_t)std::max(n, 1) * sizeof(Keypoint)));
-  HIPCHK(ctx->uncertain.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(ctx->keep.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(ctx->pos.ensure((size_t)std::max(n, 1) * sizeof(unsigned)));
-  HIPCHK(hipMemsetAsync(cnt + 3, 0, 2 * sizeof(unsigned), ctx->stream));
+  HIPCHK(ctx->status.ensure((size_t)std::max(cap, 1) * sizeof(int)));
+  HIPCHK(ctx->kp_tmp.ensure((size_t)std::max(cap, 1) * sizeof(Keypoint)));
+  HIPCHK(ctx->kp.ensure((size_t)std::max(cap, 1) * sizeof(Keypoint)));
+  HIPCHK(ctx->uncertain.ensure((size_t)std::max(cap, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->keep.ensure((size_t)std::max(cap, 1) * sizeof(unsigned)));
+  HIPCHK(ctx->pos.ensure((size_t)std::max(cap, 1) * sizeof(unsigned)));
+  HIPCHK(hipMemsetAsync(cnt + kCntUnc, 0, 2 * sizeof(unsigned), ctx->stream));
+  HIPCHK(hipMemsetAsync(cnt + kCntKp, 0, sizeof(unsigned), ctx->stream));
+  HIPCHK(hipMemsetAsync(cnt + 16, 0, 16 * sizeof(unsigned), ctx->stream));
   ctx->n_kp = 0;
   ctx->n_sing = 0;
-  if (n > 0) {
+  if (cap > 0) {
     RefineLaunch R{};
     R.cand_key = ctx->cand_key.as<unsigned>();
     R.cand_val = ctx->cand_val.as<double>();
     R.keep = ctx->has_keep ? ctx->cand_keep.as<unsigned>() : nullptr;
-    R.n = n;
+    R.n = cnt + kCntN;
+    R.cap = cap;
     R.exact_planes = ctx->dog_source == kForeign;
     R.min_blur = ctx->p.min_blur;
     R.min_interpixel_distance = ctx->p.min_interpixel_distance;
@@ -592,34 +634,38 @@ static int run_refine(sift_ctx* ctx) {
     R.uncertain = ctx->uncertain.as<unsigned>();
     R.counters = cnt;
     HIPCHK(launch_refine_fast(P, R, ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->h_counters + 3, cnt + 3, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    const unsigned nu = ctx->h_counters[3];
-    ctx->n_exact += nu;
-    if (nu) {
-      if (ctx->dog_source != kNative) return set_err(ctx, SIFT_E_STATE, "uncertain refinement without a native pyramid");
-      HIPCHK(launch_refine_exact(P, R, nu, ctx->stream));
-    }
-    HIPCHK(launch_status_to_keep(R.status, ctx->keep.as<unsigned>(), n, ctx->stream));
+    // Uncertain decisions exist only with fp32-rounded native planes.
+    if (ctx->dog_source == kNative) HIPCHK(launch_refine_exact(P, R, ctx->stream));
+    HIPCHK(launch_status_to_keep(R.status, ctx->keep.as<unsigned>(), R.n, cap, ctx->stream));
     size_t tb = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), cap,
                                             ctx->stream));
     HIPCHK(ctx->temp.ensure(tb));
     tb = ctx->temp.bytes;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), n,
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), cap,
                                             ctx->stream));
-    HIPCHK(launch_scatter_keypoints(R.status, ctx->pos.as<unsigned>(), R.kp, n, ctx->kp.as<Keypoint>(), ctx->stream));
-    unsigned last[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(&last[0], ctx->pos.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    HIPCHK(hipMemcpyAsync(&last[1], ctx->keep.as<unsigned>() + n - 1, sizeof(unsigned), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    HIPCHK(hipMemcpyAsync(ctx->h_counters + 4, cnt + 4, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    ctx->n_kp = (size_t)last[0] + last[1];
-    ctx->n_sing = ctx->h_counters[4];
+    HIPCHK(launch_scatter_keypoints(R.status, ctx->pos.as<unsigned>(), R.kp, R.n, cap, ctx->kp.as<Keypoint>(),
+                                    ctx->stream));
+    HIPCHK(launch_count_keypoints(ctx->pos.as<unsigned>(), ctx->keep.as<unsigned>(), R.n, cap, cnt + kCntKp, ctx->stream));
   }
+  HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 32 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->ext_pending) {
+    const int rc = settle_extrema(ctx);
+    if (rc) return rc;
+  }
+  const unsigned* h = ctx->h_counters;
+  if (h[kCntUnc] > (unsigned)cap) return set_err(ctx, SIFT_E_STATE, "uncertain list overflow");
+  if (h[kCntUnc] && ctx->dog_source != kNative)
+    return set_err(ctx, SIFT_E_STATE, "uncertain refinement without a native pyramid");
+  ctx->n_exact += h[kCntUnc];
+  ctx->n_kp = cap > 0 ? h[kCntKp] : 0;
+  ctx->n_sing = h[kCntSing];
+  if (std::getenv("SIFT_DEBUG_REFINE"))
+    std::fprintf(stderr,
+                 "refine uncertain %u: det %u alpha %u omega %u edge_dt %u edge_int %u round %u | iter %u %u %u %u %u\n",
+                 h[kCntUnc], h[16], h[17], h[18], h[19], h[20], h[21], h[22], h[23], h[24], h[25], h[26]);
   return SIFT_OK;
 }
 
@@ -713,9 +759,14 @@ int sift_set_candidates(sift_ctx* ctx, const sift_extremum* cand, size_t n) {
     HIPCHK(hipMemcpyAsync(ctx->cand_key.p, keys.data(), n * sizeof(unsigned), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(ctx->cand_val.p, vals.data(), n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   }
+  const unsigned n32 = (unsigned)n;
+  HIPCHK(hipMemcpyAsync(ctx->counters.as<unsigned>() + kCntN, &n32, sizeof(unsigned), hipMemcpyHostToDevice,
+                        ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->n_cand = n;
   ctx->n_slots = n;
+  ctx->slot_cap = (int)n;
+  ctx->ext_pending = false;
   ctx->has_keep = false;
   ctx->have_cand = true;
   return SIFT_OK;
@@ -738,7 +789,7 @@ int sift_refine(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out, si
   if (!ctx->have_cand) return set_err(ctx, SIFT_E_STATE, "no candidates: run sift_find_extrema first");
   HIPCHK(hipSetDevice(ctx->device));
   int rc = run_refine(ctx);
-  if (rc) return rc;
+  if (rc) return rc == kRetry ? set_err(ctx, SIFT_E_STATE, "candidate capacity overflow") : rc;
   read_stage_times(ctx, false, true);
   if (n_singular) *n_singular = ctx->n_sing;
   rc = sift_copy_keypoints(ctx, out, cap, n_out);
@@ -753,9 +804,13 @@ static int detect_common(sift_ctx* ctx, const float* img_host, const float* img_
   if (!ctx) return SIFT_E_ARG;
   int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr);
   if (rc) return rc;
-  rc = run_extrema(ctx);
-  if (rc) return rc;
-  rc = run_refine(ctx);
+  // One host synchronisation per image; a capacity overflow (first images)
+  // grows the buffers and reruns extrema + refinement.
+  do {
+    rc = launch_extrema_stage(ctx);
+    if (rc) return rc;
+    rc = run_refine(ctx);
+  } while (rc == kRetry);
   if (rc) return rc;
   float a = 0, b = 0;
   (void)hipEventSynchronize(ctx->ev[6]);

@@ -272,47 +272,55 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
       const int b = __ffsll((long long)word) - 1;
       word &= word - 1;
       const int x = xw * kXW + b;
-      E.keys[pos] = kbase + (unsigned)x;
-      E.value[pos] = (double)Dc[x];
-      E.keep[pos] = 1u;
+      if (pos < E.cap) {
+        E.keys[pos] = kbase + (unsigned)x;
+        E.value[pos] = (double)Dc[x];
+        E.keep[pos] = 1u;
+      }
       ++pos;
     }
     base += __shfl(inc, 63);
   }
 }
 
-// One 64-thread block (one wave) per ambiguous candidate: fp64 recompute of
-// the 3x3x3 patch decides extremum and contrast exactly.
+// One 64-thread block (one wave) per ambiguous candidate, persistent over the
+// device-side count: fp64 recompute of the 3x3x3 patch decides extremum and
+// contrast exactly.
 __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const ExactLaunch X) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const unsigned key = X.amb_keys[blockIdx.x];
-  // position of key in the ordered candidate list (binary search)
-  unsigned lo = 0, hi = X.n;
-  while (lo < hi) {
-    const unsigned mid = (lo + hi) >> 1;
-    if (X.keys[mid] < key) lo = mid + 1; else hi = mid;
-  }
-  const unsigned idx = lo;
-  int o, s, y, x;
-  decode_key(P, key, o, s, y, x);
-  double* d27 = smem;
-  double* Lbuf = smem + 32;
-  double* sh = smem + 32 + 40;
-  wave_dog_patch(P, o, s, y, x, sh, Lbuf, d27);
-  if (threadIdx.x == 0 && idx < X.n && X.keys[idx] == key) {
-    const double v = d27[13];
-    bool gt = false, lt = false;
-    for (int q = 0; q < 27; ++q) {
-      if (q == 13) continue;
-      gt |= d27[q] >= v;  // a neighbour >= v rules out a strict maximum
-      lt |= d27[q] <= v;
+  const unsigned n_amb = min(X.counters[0], X.amb_cap);
+  const unsigned n = min(*X.n, X.cap);
+  for (unsigned j = blockIdx.x; j < n_amb; j += gridDim.x) {
+    const unsigned key = X.amb_keys[j];
+    // position of key in the ordered candidate list (binary search)
+    unsigned lo = 0, hi = n;
+    while (lo < hi) {
+      const unsigned mid = (lo + hi) >> 1;
+      if (X.keys[mid] < key) lo = mid + 1; else hi = mid;
     }
-    const bool ext = !gt || !lt;
-    const bool cand = ext && fabs(v) >= P.pix_thr;
-    X.keep[idx] = cand ? 1u : 0u;
-    X.value[idx] = v;
-    if (ext && !cand) atomicAdd(&X.counters[1], 1u);
-    if (!cand) atomicAdd(&X.counters[2], 1u);  // dropped entries
+    const unsigned idx = lo;
+    int o, s, y, x;
+    decode_key(P, key, o, s, y, x);
+    double* d27 = smem;
+    double* Lbuf = smem + 32;
+    double* sh = smem + 32 + 40;
+    wave_dog_patch(P, o, s, y, x, sh, Lbuf, d27);
+    if (threadIdx.x == 0 && idx < n && X.keys[idx] == key) {
+      const double v = d27[13];
+      bool gt = false, lt = false;
+      for (int q = 0; q < 27; ++q) {
+        if (q == 13) continue;
+        gt |= d27[q] >= v;  // a neighbour >= v rules out a strict maximum
+        lt |= d27[q] <= v;
+      }
+      const bool ext = !gt || !lt;
+      const bool cand = ext && fabs(v) >= P.pix_thr;
+      X.keep[idx] = cand ? 1u : 0u;
+      X.value[idx] = v;
+      if (ext && !cand) atomicAdd(&X.counters[1], 1u);
+      if (!cand) atomicAdd(&X.counters[2], 1u);  // dropped entries
+    }
+    __syncthreads();  // smem is reused by the next key
   }
 }
 
@@ -349,9 +357,9 @@ size_t exact_lds_bytes(const Pyramid& P) {
   return sizeof(double) * (size_t)(32 + 40 + exact_scratch_doubles(rmax));
 }
 
-hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, unsigned n_amb, hipStream_t st) {
-  if (n_amb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_exact_extrema, dim3(n_amb), dim3(64), exact_lds_bytes(P), st, P, X);
+hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, hipStream_t st) {
+  const unsigned grid = std::max(1u, std::min(X.amb_cap, 4096u));
+  hipLaunchKernelGGL(k_exact_extrema, dim3(grid), dim3(64), exact_lds_bytes(P), st, P, X);
   return hipGetLastError();
 }
 

@@ -52,12 +52,15 @@ struct EmitLaunch {
   unsigned* keys;                // ordered candidate keys
   double* value;
   unsigned* keep;
+  unsigned cap;                  // slots in keys/value/keep (overflow is detected by the host)
 };
 
 struct ExactLaunch {
-  const unsigned* amb_keys;
+  const unsigned* amb_keys;      // counters[0] of them (at most amb_cap stored)
+  unsigned amb_cap;
   const unsigned* keys;          // ordered candidates
-  unsigned n;
+  const unsigned* n;             // device: number of candidates
+  unsigned cap;
   unsigned* keep;
   double* value;
   unsigned* counters;
@@ -67,7 +70,8 @@ struct RefineLaunch {
   const unsigned* cand_key;
   const double* cand_val;
   const unsigned* keep;  // nullptr = every entry is a candidate
-  int n;
+  const unsigned* n;     // device: number of entries (<= cap)
+  int cap;
   int exact_planes;
   double min_blur, min_interpixel_distance;
   int* status;        // per candidate kRef*
@@ -86,16 +90,21 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st);
 inline int extrema_words_per_row(int w) { return (w + kXW - 1) / kXW; }
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st);
 // One wave per ambiguous candidate: fp64 pointwise recompute of the 3x3x3 DoG patch.
-hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, unsigned n_amb, hipStream_t st);
+// Persistent grid over the device-side count of ambiguous keys (no host sync).
+hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, hipStream_t st);
 
 hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream_t st);
-hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, unsigned n_uncertain,
-                               hipStream_t st);
+hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, hipStream_t st);
 
 // Order-preserving compaction helpers.
+// Entries i >= *n (device count) of the cap-sized arrays are inactive.
 hipError_t launch_scatter_keypoints(const int* status, const unsigned* pos, const Keypoint* kp,
-                                    int n, Keypoint* out, hipStream_t st);
-hipError_t launch_status_to_keep(const int* status, unsigned* keep, int n, hipStream_t st);
+                                    const unsigned* n, int cap, Keypoint* out, hipStream_t st);
+hipError_t launch_status_to_keep(const int* status, unsigned* keep, const unsigned* n, int cap,
+                                 hipStream_t st);
+// out = pos[n-1] + keep[n-1] (0 if n == 0): the number of keypoints.
+hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, const unsigned* n, int cap,
+                                  unsigned* out, hipStream_t st);
 
 size_t exact_lds_bytes(const Pyramid& P);
 

@@ -37,6 +37,7 @@ __device__ __forceinline__ double round_margin(double v) {
 struct StepOut {
   int state;         // 0 continue (moved), 1 keep, 2 discard, 3 singular
   bool uncertain;
+  unsigned why;      // diagnostic: which decisions were uncertain (bits 0..5)
   double a[3];
   double omega;
   int s, m, n;       // position after the step (moved) or of the keypoint
@@ -44,13 +45,21 @@ struct StepOut {
 
 // One iteration of background.js:480-664 on the patch d[k][a][c]
 // (k: scale s-1+k, a: row m-1+a, c: col n-1+c).  `delta` bounds the error of
-// every patch value (0 = exact), `dval` that of the candidate value.
+// every patch value (0 = exact), `dval` that of the candidate value.  With
+// delta > 0 every decision carries an error bound: gradient entries are off
+// by <= delta, Hessian entries by <= 4 delta (diagonal worst case); the
+// inverse is bounded through ||H^-1 E|| <= kappa < 1/2 (perturbation lemma),
+// and each bound gets a factor kSafe of slack.  A decision inside its bound
+// sets `uncertain`.  On the last iteration (`last`) a move discards, so the
+// new position's rounding does not matter.
 __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int n, double value,
                                       double delta, double dval, int S, int ND, int h, int w,
-                                      double thr) {
+                                      double thr, bool last) {
+  constexpr double kSafe = 2.0;
 #define DP(k, a, c) d[(k) * 9 + (a) * 3 + (c)]
   StepOut R;
   R.uncertain = false;
+  R.why = 0;
   const double cc = DP(1, 1, 1);
   const double g0 = (DP(2, 1, 1) - DP(0, 1, 1)) / 2;
   const double g1 = (DP(1, 2, 1) - DP(1, 0, 1)) / 2;
@@ -73,14 +82,19 @@ __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int 
       mn[i][j] = (M[r0][c0] * M[r1][c1]) - (M[r0][c1] * M[r1][c0]);
     }
   const double det = ((M[0][0] * mn[0][0]) - (M[0][1] * mn[0][1])) + (M[0][2] * mn[0][2]);
-  const double dH = 4 * delta;  // |error| of every Hessian entry (diagonal worst case)
+  const double dG = delta, dH = 4 * delta;
   if (delta > 0) {
-    double cof1 = 0;
+    double cof1 = 0, hmax = 0;
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) cof1 += fabs(mn[i][j]);
-    if (fabs(fabs(det) - 2.220446049250313e-16) <= 16 * (cof1 * dH + 1e-300)) R.uncertain = true;
+      for (int j = 0; j < 3; ++j) {
+        cof1 += fabs(mn[i][j]);
+        hmax = fmax(hmax, fabs(M[i][j]));
+      }
+    // d det <= sum |cofactor| dH + second order (3 (2 hmax + dH) dH^2 ... )
+    const double Edet = kSafe * (cof1 * dH + 9 * (2 * hmax + dH) * dH * dH) + 1e-300;
+    if (fabs(fabs(det) - 2.220446049250313e-16) <= Edet) R.uncertain = true, R.why |= 1;
   }
   if (fabs(det) < 2.220446049250313e-16) {
     R.state = 3;
@@ -108,47 +122,65 @@ __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int 
     R.a[i] = r;
   }
   const double a1 = fabs(R.a[0]) + fabs(R.a[1]) + fabs(R.a[2]);
-  // First-order error of alpha = -H^-1 g under |dg| <= delta, |dH| <= 4 delta.
-  const double Ea = delta > 0 ? 16 * inv_norm * (delta + dH * a1) + 1e-300 : 0.0;
+  // |d alpha| <= ||H^-1|| (dG + ||E|| |alpha|) / (1 - kappa),  ||E||_inf <= 3 dH.
+  double Ea = 0.0;
   if (delta > 0) {
+    const double kappa = inv_norm * 3 * dH;
+    if (kappa >= 0.5) {
+      R.uncertain = true, R.why |= 2;
+      Ea = 1e300;
+    } else {
+      Ea = kSafe * inv_norm * (dG + 3 * dH * a1) / (1 - kappa) + 1e-300;
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      if (fabs(fabs(R.a[i]) - 0.6) <= Ea) R.uncertain = true;
+      if (fabs(fabs(R.a[i]) - 0.6) <= Ea) R.uncertain = true, R.why |= 2;
   }
   if (fabs(R.a[0]) < 0.6 && fabs(R.a[1]) < 0.6 && fabs(R.a[2]) < 0.6) {
     const double omega = value + (((0.5 * R.a[0]) * g0) + ((0.5 * R.a[1]) * g1) + ((0.5 * R.a[2]) * g2));
     R.omega = omega;
     R.s = s; R.m = m; R.n = n;
     if (delta > 0 || dval > 0) {
-      const double Eo = 16 * (dval + 0.5 * (Ea * (fabs(g0) + fabs(g1) + fabs(g2)) + a1 * delta)) + 1e-300;
-      if (fabs(fabs(omega) - thr) <= Eo) R.uncertain = true;
+      const double Eo = kSafe * (dval + 0.5 * (Ea * (fabs(g0) + fabs(g1) + fabs(g2)) + (a1 + 3 * Ea) * dG)) + 1e-300;
+      if (fabs(fabs(omega) - thr) <= Eo) R.uncertain = true, R.why |= 4;
     }
     if (fabs(omega) < thr) { R.state = 2; return R; }
     const double tr = (0 + h22) + h33;
     const double dt = (h22 * h33) - (h23 * h23);
     const double edgeness = (tr * tr) / dt;
     if (delta > 0) {
-      // Interval bound on tr^2/det2 with |dtr| <= 8 delta, |ddet2| <= (|h22|+|h33|) 4 delta + 2|h23| delta.
-      const double Etr = 16 * 8 * delta;
-      const double Edt = 16 * ((fabs(h22) + fabs(h33)) * dH + 2 * fabs(h23) * delta) + 1e-300;
+      // Interval bound on tr^2/det2: |dtr| <= 2 dH, |ddet2| <= (|h22|+|h33|) dH + 2|h23| dG + dH^2 + dG^2.
+      const double Etr = kSafe * 2 * dH;
+      const double Edt = kSafe * ((fabs(h22) + fabs(h33)) * dH + 2 * fabs(h23) * dG + dH * dH + dG * dG) + 1e-300;
       if (fabs(dt) <= Edt) {
         R.uncertain = true;
+        R.why |= 8;
       } else {
         const double t_hi = fabs(tr) + Etr, t_lo = fmax(0.0, fabs(tr) - Etr);
         const double d_lo = fabs(dt) - Edt, d_hi = fabs(dt) + Edt;
         double e_lo, e_hi;
         if (dt > 0) { e_lo = t_lo * t_lo / d_hi; e_hi = t_hi * t_hi / d_lo; }
         else { e_lo = -(t_hi * t_hi / d_lo); e_hi = -(t_lo * t_lo / d_hi); }
-        if (e_lo <= 12.1 && 12.1 <= e_hi) R.uncertain = true;
+        if (e_lo <= 12.1 && 12.1 <= e_hi) R.uncertain = true, R.why |= 16;
       }
     }
     if (edgeness > ((10 + 1) * (10 + 1)) / 10.0) { R.state = 2; return R; }
     R.state = 1;
     return R;
   }
+  if (last) {  // the reference gives up after 5 moves: discard wherever it lands
+    R.state = 2;
+    return R;
+  }
   const double vs = s + R.a[0], vm = m + R.a[1], vn = n + R.a[2];
-  if (delta > 0 && (round_margin(vs) <= Ea || round_margin(vm) <= Ea || round_margin(vn) <= Ea))
-    R.uncertain = true;
+  if (delta > 0 && (round_margin(vs) <= Ea || round_margin(vm) <= Ea || round_margin(vn) <= Ea)) {
+    // Rounding is monotone: if every position within the bound leaves the
+    // refinable interior in some coordinate, the move discards either way.
+    const bool out_s = js_round(vs + Ea) < 1 || js_round(vs - Ea) >= ND - 1;
+    const bool out_m = js_round(vm + Ea) < 1 || js_round(vm - Ea) >= h - 1;
+    const bool out_n = js_round(vn + Ea) < 1 || js_round(vn - Ea) >= w - 1;
+    if (!(out_s || out_m || out_n)) R.uncertain = true, R.why |= 32;
+  }
   R.s = (int)js_round(vs);
   R.m = (int)js_round(vm);
   R.n = (int)js_round(vn);
@@ -175,10 +207,11 @@ __device__ inline void make_keypoint(Keypoint& k, int o, const StepOut& R, int S
 
 __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const RefineLaunch L) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n = (int)min(*L.n, (unsigned)L.cap);
   bool unc = false;
-  if (i < L.n && L.keep && !L.keep[i]) {
+  if (i < n && L.keep && !L.keep[i]) {
     L.status[i] = kRefDiscard;
-  } else if (i < L.n) {
+  } else if (i < n) {
     int o, s, m, n;
     decode_key(P, L.cand_key[i], o, s, m, n);
     const Octave& oc = P.oct[o];
@@ -203,8 +236,14 @@ __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const Refi
           }
       // fp32 rounding of the fp64 value (<= |v| 2^-24) plus fp64 noise vs the reference.
       const double delta = L.exact_planes ? 0.0 : mx * (0x1p-24 + 0x1p-40);
-      const StepOut R = refine_step(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr);
-      if (R.uncertain) { unc = true; break; }
+      const StepOut R = refine_step(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4);
+      if (R.uncertain) {
+        unc = true;
+        for (int b = 0; b < 6; ++b)
+          if ((R.why >> b) & 1u) atomicAdd(&L.counters[16 + b], 1u);
+        atomicAdd(&L.counters[22 + min(it, 4)], 1u);
+        break;
+      }
       if (R.state == 3) { status = kRefSingular; break; }
       if (R.state == 2) { status = kRefDiscard; break; }
       if (R.state == 1) {
@@ -228,84 +267,104 @@ __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const Refi
   }
 }
 
-// One wave per uncertain candidate: exact fp64 patches, lane 0 decides.
+// One wave per uncertain candidate (persistent over the device-side count):
+// exact fp64 patches, lane 0 decides.
 __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const RefineLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int pos[4];
-  const unsigned i = L.uncertain[blockIdx.x];
-  int o, s, m, n;
-  decode_key(P, L.cand_key[i], o, s, m, n);
-  const Octave& oc = P.oct[o];
-  double* d27 = smem;
-  double* Lbuf = smem + 32;
-  double* sh = smem + 32 + 40;
-  double value = 0;
-  int status = kRefDiscard;
-  for (int it = 0; it < 5; ++it) {
-    wave_dog_patch(P, o, s, m, n, sh, Lbuf, d27);
-    if (threadIdx.x == 0) {
-      if (it == 0) value = d27[13];  // exact fp64 candidate value (:565 uses it)
-      const StepOut R = refine_step(d27, o, s, m, n, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr);
-      int cont = 0;
-      if (R.state == 3) status = kRefSingular;
-      else if (R.state == 2) status = kRefDiscard;
-      else if (R.state == 1) {
-        status = kRefKeep;
-        make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance);
-      } else {
-        cont = 1;
-        pos[0] = R.s; pos[1] = R.m; pos[2] = R.n;
+  const unsigned nu = min(L.counters[3], (unsigned)L.cap);
+  for (unsigned j = blockIdx.x; j < nu; j += gridDim.x) {
+    const unsigned i = L.uncertain[j];
+    int o, s, m, n;
+    decode_key(P, L.cand_key[i], o, s, m, n);
+    const Octave& oc = P.oct[o];
+    double* d27 = smem;
+    double* Lbuf = smem + 32;
+    double* sh = smem + 32 + 40;
+    double value = 0;
+    int status = kRefDiscard;
+    for (int it = 0; it < 5; ++it) {
+      wave_dog_patch(P, o, s, m, n, sh, Lbuf, d27);
+      if (threadIdx.x == 0) {
+        if (it == 0) value = d27[13];  // exact fp64 candidate value (:565 uses it)
+        const StepOut R = refine_step(d27, o, s, m, n, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr, it == 4);
+        int cont = 0;
+        if (R.state == 3) status = kRefSingular;
+        else if (R.state == 2) status = kRefDiscard;
+        else if (R.state == 1) {
+          status = kRefKeep;
+          make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance);
+        } else {
+          cont = 1;
+          pos[0] = R.s; pos[1] = R.m; pos[2] = R.n;
+        }
+        pos[3] = cont;
       }
-      pos[3] = cont;
+      __syncthreads();
+      const int cont = pos[3];
+      s = pos[0]; m = pos[1]; n = pos[2];
+      __syncthreads();
+      if (!cont) break;
     }
-    __syncthreads();
-    if (!pos[3]) break;
-    s = pos[0]; m = pos[1]; n = pos[2];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    L.status[i] = status;
-    if (status == kRefSingular) atomicAdd(&L.counters[4], 1u);
+    if (threadIdx.x == 0) {
+      L.status[i] = status;
+      if (status == kRefSingular) atomicAdd(&L.counters[4], 1u);
+    }
   }
 }
 
 __global__ __launch_bounds__(256) void k_status_to_keep(const int* __restrict__ status,
-                                                        unsigned* __restrict__ keep, int n) {
+                                                        unsigned* __restrict__ keep,
+                                                        const unsigned* __restrict__ n, int cap) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) keep[i] = status[i] == kRefKeep ? 1u : 0u;
+  if (i < cap) keep[i] = (i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void k_scatter_kp(const int* __restrict__ status,
                                                     const unsigned* __restrict__ pos,
-                                                    const Keypoint* __restrict__ kp, int n,
+                                                    const Keypoint* __restrict__ kp,
+                                                    const unsigned* __restrict__ n, int cap,
                                                     Keypoint* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n && status[i] == kRefKeep) out[pos[i]] = kp[i];
+  if (i < cap && i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep) out[pos[i]] = kp[i];
+}
+
+__global__ void k_count_kp(const unsigned* __restrict__ pos, const unsigned* __restrict__ keep,
+                           const unsigned* __restrict__ n, unsigned cap, unsigned* __restrict__ out) {
+  const unsigned m = min(*n, cap);
+  *out = m ? pos[m - 1] + keep[m - 1] : 0u;
 }
 
 hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream_t st) {
-  if (R.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_refine_fast, dim3((R.n + 255) / 256), dim3(256), 0, st, P, R);
+  if (R.cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_refine_fast, dim3((R.cap + 255) / 256), dim3(256), 0, st, P, R);
   return hipGetLastError();
 }
 
-hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, unsigned n_uncertain,
-                               hipStream_t st) {
-  if (n_uncertain == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_refine_exact, dim3(n_uncertain), dim3(64), exact_lds_bytes(P), st, P, R);
+hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, hipStream_t st) {
+  if (R.cap <= 0) return hipSuccess;
+  const int grid = std::max(1, std::min(R.cap, 8192));
+  hipLaunchKernelGGL(k_refine_exact, dim3(grid), dim3(64), exact_lds_bytes(P), st, P, R);
   return hipGetLastError();
 }
 
-hipError_t launch_status_to_keep(const int* status, unsigned* keep, int n, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_status_to_keep, dim3((n + 255) / 256), dim3(256), 0, st, status, keep, n);
+hipError_t launch_status_to_keep(const int* status, unsigned* keep, const unsigned* n, int cap,
+                                 hipStream_t st) {
+  if (cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_status_to_keep, dim3((cap + 255) / 256), dim3(256), 0, st, status, keep, n, cap);
   return hipGetLastError();
 }
 
 hipError_t launch_scatter_keypoints(const int* status, const unsigned* pos, const Keypoint* kp,
-                                    int n, Keypoint* out, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter_kp, dim3((n + 255) / 256), dim3(256), 0, st, status, pos, kp, n, out);
+                                    const unsigned* n, int cap, Keypoint* out, hipStream_t st) {
+  if (cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_kp, dim3((cap + 255) / 256), dim3(256), 0, st, status, pos, kp, n, cap, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, const unsigned* n, int cap,
+                                  unsigned* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_count_kp, dim3(1), dim3(1), 0, st, pos, keep, n, (unsigned)cap, out);
   return hipGetLastError();
 }
 
