@@ -71,6 +71,7 @@ struct sift_ctx {
   bool has_keep = false;    // slots carry keep flags
   // device memory
   DBuf img, seeds, gauss, dog, wts;
+  DBuf base0;                                  // materialised octave-0 base (large radii only)
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
   DBuf keep, pos;                              // keypoint compaction
@@ -178,7 +179,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   if (!ctx) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
+  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->counters, &ctx->temp};
@@ -275,7 +276,7 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
     }
   }
   if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");
-  // LDS feasibility of the Gaussian kernel (strip of min(h, 32+2R) fp64 rows).
+  // LDS feasibility of the Gaussian kernel (two strips of 32 rows x (76 + 2R) fp64).
   for (int o = 0; o < O; ++o)
     if (gauss_lds_bytes(P, o) > 160 * 1024)
       return set_err(ctx, SIFT_E_UNSUPPORTED, "blur radius too large for one LDS strip");
@@ -326,10 +327,17 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   P.seeds = ctx->seeds.as<double>();
   P.dog = ctx->dog.as<float>();
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
+  const double* base0 = nullptr;
+  if (gauss_needs_base0(P)) {
+    HIPCHK(ctx->base0.ensure((size_t)P.oct[0].h * P.oct[0].w * sizeof(double)));
+    HIPCHK(launch_upsample_base(P, ctx->base0.as<double>(), ctx->stream));
+    base0 = ctx->base0.as<double>();
+  }
   for (int o = 0; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
     GaussLaunch L{};
     L.o = o;
+    L.base = o == 0 ? base0 : ctx->seeds.as<double>() + oc.seed_off;
     L.gauss = keep_gauss ? ctx->gauss.as<float>() + oc.gauss_off : nullptr;
     L.dog = ctx->dog.as<float>() + oc.dog_off;
     L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off : nullptr;

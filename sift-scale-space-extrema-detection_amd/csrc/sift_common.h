@@ -15,10 +15,7 @@ namespace sift {
 
 constexpr int kMaxOctaves = 12;
 constexpr int kMaxScales = 12;   // S+3 <= kMaxScales  (S <= 9)
-constexpr int kWPad = 8;         // zero taps on both sides of every weight vector
-constexpr int kTX = 64;          // Gaussian tile width  (one wave of columns)
-constexpr int kTY = 32;          // Gaussian tile height (4 waves x 8 rows)
-constexpr int kVT = 8;           // vertical outputs per thread (register sliding window)
+constexpr int kWPad = 16;        // zero taps on both sides of every weight vector
 
 // fp64 in the constant address space: uniform indices become scalar loads.
 typedef __attribute__((address_space(4))) const double cdouble;

@@ -6,38 +6,40 @@
 //
 // The reference convolves every scale of an octave with a full 2D kernel of
 // the SAME octave base (the blur is not incremental, background.js:173-177).
-// The 2D kernel is exactly separable (w(i) w(j), sift.js:22-67).  Each 64x32
-// output tile stages its base region once in LDS (fp64, replicated edges) and
-// then, per scale:
-//   vertical pass   base region -> fp64 LDS strip V[32][64+2r]: an 8-row
-//                   register sliding window per column;
-//   horizontal pass strip -> 8 outputs per thread (4 rows x 2 adjacent
-//                   columns from 16-byte reads of aligned column pairs);
-//   epilogue        L_s (fp32), DoG L_{s-1} - L_s formed in fp64 and rounded
-//                   once (fp32), and for s == S the fp64 seed of the next
+// The 2D kernel is exactly separable (w(i) w(j), sift.js:22-67).  One block
+// owns a 64x32 output tile and walks all scales of the octave over it:
+//
+//   vertical pass   base -> fp64 LDS strip V[32][...]: one lane per column,
+//                   an 8-row register window per wave (8 accumulators, every
+//                   base value loaded once per window);
+//   horizontal pass strip -> 4 adjacent columns x 2 rows per lane, the row
+//                   window read with 16-byte LDS loads;
+//   epilogue        L_s and DoG L_{s-1} - L_s (formed in fp64, rounded once)
+//                   as float4 stores; for s == S the fp64 seed of the next
 //                   octave (background.js:114-118).
-// Radii 0..kRT run fully unrolled code with exactly 2r+1 taps per output
-// (taps in SGPRs); larger radii use a zero-padded runtime loop.  When the
-// base region does not fit (large radii, small octaves) the vertical pass
-// reads the base from global memory (L1/L2) instead.
+//
+// The strips are double-buffered: the vertical pass of scale s+1 runs
+// between the horizontal pass and the stores of scale s, one barrier per
+// scale.  Radii 0..kUR run fully unrolled code specialised on the radius
+// (every tap an SGPR operand of v_fma_f64, every load an immediate-offset
+// LDS read or a scalar-row global read); larger radii run 8-wide chunks over
+// zero-padded taps (fma(0, v, acc) == acc, so the results are identical).
 //
 // Octave 0's base is the 2x nearest-neighbour upsample of the input
-// (background.js:84): B[y][x] = I[clamp(y)>>1][clamp(x)>>1], never
-// materialised: the tile stages input pixels, and the vertical sums (which
-// depend on x only through x>>1) are computed once per input column and
-// written to both strip columns 2k, 2k+1 -- the same operations on the same
-// data, i.e. a pure common subexpression.
+// (background.js:84): B[y][x] = I[clamp(y>>1)][clamp(x>>1)], never
+// materialised.  The block stages its input region (fp64) in LDS; the
+// vertical pass runs on input columns only (the vertical sums depend on x
+// only through x>>1) and the horizontal pass reads the half-resolution strip
+// through the same index map -- the same operations on the same values as a
+// full-resolution pass, half the loads.
 //
-// Every output pixel runs the same operation sequence on its clamped
-// neighbourhood (translation invariant, like the reference's 2D sum), so
-// pixels with identical neighbourhoods get bit-identical values and fp32 ties
-// mean what fp64 ties mean in the reference.  sift_exact.h recomputes single
-// pixels with the same sums in the same fma order.
+// Every output pixel runs the same fma chain (taps in increasing order,
+// vertical then horizontal, starting from 0.0) on its clamped neighbourhood:
+// the result is translation invariant like the reference's 2D sum, and
+// sift_exact.h reproduces any single pixel bit for bit.
 //
 // Roofline: HBM-bound on the plane stores: per octave pixel 4(S+3) + 4(S+2)
-// bytes written (+2 for the fp64 seed) against 1 (octave 0) or 8 bytes of
-// base read.  fp64 VALU: 2(2r+1) FMAs per pixel and scale (octave 0: the
-// vertical half is shared by column pairs) plus the 2r-column halo.
+// bytes written against 1 (octave 0) or 8 bytes of base read.
 #include <cstdlib>
 #include <utility>
 
@@ -46,270 +48,426 @@
 
 namespace sift {
 
-constexpr int kRT = -1;  // radii with unrolled code paths (-1: none; the generic loops are near-exact)
+constexpr int kGX = 64;              // tile columns
+constexpr int kGY = 32;              // tile rows: 4 waves x 8
+constexpr int kUR = 16;              // radii with unrolled code
+constexpr int kCG = kGX / 4;         // column groups of 4 outputs (16)
+constexpr int kRS = 64 / kCG;        // row sub-groups per wave (4)
+constexpr int kNR = 8 / kRS;         // rows per lane in the horizontal pass (2)
+constexpr int kBW0 = kGX / 2 + kUR + 4;  // staged octave-0 region width (input columns)
+constexpr int kPFV = 6;              // rows in flight, vertical pass from global memory
+constexpr int kPFL = 4;              // rows in flight, vertical pass from LDS
+constexpr int kPFH = 3;              // 16-byte reads in flight, horizontal pass
 
-struct TileCtx {
-  const Pyramid* P;
-  const Octave* oc;
-  double* sV;    // strip [32][VW]
-  double* sB;    // staged base region [BR][BW] (nullptr: read global)
-  int h, w, R, VW, BW, rlo, x0, y0, lane, wv;
-  int kb_all;    // octave 0: first staged input column
+__host__ __device__ constexpr int fl2(int a) { return a >> 1; }   // floor(a / 2)
+__host__ __device__ constexpr int cl2(int a) { return (a + 1) >> 1; }  // ceil(a / 2), a >= 0
+
+struct GTile {
+  int h, w, x0, y0;
+  int lane, wv;        // wv wave-uniform (SGPR)
+  int cg, rs;          // horizontal mapping
+  int sw;              // strip stride
+  int hrm;             // octave 0: ceil(RM / 2) of the staged region
+  const double* S0;    // octave 0: staged input region [..][kBW0]
+  __amdgpu_buffer_rsrc_t rsrc;  // o >= 1 (or materialised octave 0): fp64 base plane h x w
 };
 
-template <bool OCT0, bool STAGED, int RAD>
-__device__ __forceinline__ void vert_pass(const TileCtx& T, const cdouble* wp, int r_rt) {
-  const int r = RAD >= 0 ? RAD : r_rt;
-  const int h = T.h, w = T.w;
-  const int ty = T.wv * kVT;
-  const int yb = T.y0 + ty - r;
-  const Pyramid& P = *T.P;
-  // columns: o>=1 -> strip columns c = 0 .. 63+2r (x = x0-r+c);
-  //          o==0 -> input columns k = kb .. ke (strip columns 2k-(x0-r), +1)
-  const int kb = (T.x0 - r) >> 1;
-  const int ncols = OCT0 ? (((T.x0 + kTX - 1 + r) >> 1) - kb + 1) : (kTX + 2 * r);
-  for (int cb = 0; cb < ncols; cb += 64) {
-    const int col = cb + T.lane;
-    // source column: staged index or global column
-    int scol;
-    if (STAGED) scol = OCT0 ? min(kb + col - T.kb_all, T.BW - 1) : min(col + T.R - r, T.BW - 1);
-    else scol = OCT0 ? clampi(kb + col, 0, P.W - 1) : clampi(T.x0 - r + col, 0, w - 1);
-    auto src = [&](int j) -> double {
-      const int yy = clampi(yb + j, 0, h - 1);
-      if (STAGED) return T.sB[((OCT0 ? (yy >> 1) : yy) - T.rlo) * T.BW + scol];
-      if (OCT0) return (double)P.img[(long long)(yy >> 1) * P.img_stride + scol];
-      return P.seeds[T.oc->seed_off + (long long)yy * w + scol];
-    };
-    double acc[kVT];
+__device__ __forceinline__ double load_f64(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+
+// ---------------------------------------------------------------------------
+// Vertical pass, base plane in global memory (L1/L2): V[8 wv + t][c] =
+// sum_k w_k B[y0 + 8 wv + t - r + k][x0 - r + c], c in [0, 64 + 2r).
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void vert_glob(const GTile& T, const cdouble* wp, double* V) {
+  constexpr int NC = kGX + 2 * R;
+  constexpr int NJ = 2 * R + 8;
+  const int yb = __builtin_amdgcn_readfirstlane(T.y0 + 8 * T.wv - R);
 #pragma unroll
-    for (int t = 0; t < kVT; ++t) acc[t] = 0.0;
-    if constexpr (RAD >= 0) {
-      double v = src(0);
+  for (int cb = 0; cb < NC; cb += 64) {
+    const int c = cb + T.lane;
+    if (cb + 64 <= NC || c < NC) {
+      // Buffer loads: the column is a per-lane byte offset, the row a
+      // wave-uniform SGPR offset (no per-row address arithmetic in VGPRs).
+      const int xoff = clampi(T.x0 - R + c, 0, T.w - 1) * 8;
+      auto ld = [&](int j) -> double {
+        int yy = yb + j;
+        asm volatile("" : "+s"(yy));  // computed at its use: no early SGPR offsets for every row
+        return load_f64(T.rsrc, xoff, clampi(yy, 0, T.h - 1) * T.w * 8);
+      };
+      double acc[8], v[NJ];
 #pragma unroll
-      for (int j = 0; j < 2 * RAD + kVT; ++j) {
-        const double vn = j + 1 < 2 * RAD + kVT ? src(j + 1) : 0.0;  // one row ahead
+      for (int t = 0; t < 8; ++t) acc[t] = 0.0;
 #pragma unroll
-        for (int t = 0; t < kVT; ++t) {
+      for (int j = 0; j < kPFV && j < NJ; ++j) v[j] = ld(j);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (j + kPFV < NJ) v[j + kPFV] = ld(j + kPFV);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
           const int k = j - t;
-          if (k >= 0 && k <= 2 * RAD) acc[t] = fma((double)wp[k], v, acc[t]);
+          if (k >= 0 && k <= 2 * R) acc[t] = fma((double)wp[k], v[j], acc[t]);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        v = vn;
+        __builtin_amdgcn_sched_barrier(0);  // keep the window short (no hoisting of every load)
       }
-    } else {
-#pragma unroll 8
-      for (int j = 0; j < 2 * r + kVT; ++j) {
-        const double v = src(j);
+      double* dst = V + 8 * T.wv * T.sw + c;
 #pragma unroll
-        for (int t = 0; t < kVT; ++t) acc[t] = fma(wp[j - t], v, acc[t]);  // zero-padded taps
-      }
-    }
-    if (col < ncols) {
-      double* dst = T.sV + ty * T.VW;
-      if (OCT0) {
-        const int u = 2 * (kb + col) - (T.x0 - r);  // strip column of x = 2k
-#pragma unroll
-        for (int t = 0; t < kVT; ++t) {
-          if (u >= 0 && u < kTX + 2 * r) dst[t * T.VW + u] = acc[t];
-          if (u + 1 >= 0 && u + 1 < kTX + 2 * r) dst[t * T.VW + u + 1] = acc[t];
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < kVT; ++t) dst[t * T.VW + col] = acc[t];
-      }
+      for (int t = 0; t < 8; ++t) dst[t * T.sw] = acc[t];
     }
   }
 }
 
-// Horizontal pass for one scale: lane -> column pair p = lane & 31 (output
-// columns x0+2p, x0+2p+1), rows ty + 2m + (lane >> 5), m = 0..3.
-// out[2m + c] = sum_i w_i V[row][2p + c + i], taps in increasing i.
-template <int RAD>
-__device__ __forceinline__ void horz_pass(const TileCtx& T, const cdouble* wp, int r_rt, double (&out)[kVT]) {
-  const int r = RAD >= 0 ? RAD : r_rt;
-  const int p = T.lane & 31, half = T.lane >> 5;
-  const double* base = T.sV + (T.wv * kVT + half) * T.VW + 2 * p;
+__device__ __forceinline__ void vert_glob_gen(const GTile& T, int r, const cdouble* wp, double* V) {
+  const int NC = kGX + 2 * r, NJ = 2 * r + 8;
+  const int yb = T.y0 + 8 * T.wv - r;
+  for (int cb = 0; cb < NC; cb += 64) {
+    const int c = cb + T.lane;
+    const int xoff = clampi(T.x0 - r + min(c, NC - 1), 0, T.w - 1) * 8;
+    double acc[8];
 #pragma unroll
-  for (int q = 0; q < kVT; ++q) out[q] = 0.0;
-  if constexpr (RAD >= 0) {
-    // Software-pipelined one column pair ahead; the scheduling barriers keep
-    // the compiler from hoisting the whole unrolled window (register blow-up).
-    double2 cur[kVT / 2], nxt[kVT / 2];
+    for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+    for (int jb = 0; jb < NJ; jb += 8) {
+      double v[8];
 #pragma unroll
-    for (int m = 0; m < kVT / 2; ++m) cur[m] = *reinterpret_cast<const double2*>(base + 2 * m * T.VW);
+      for (int k = 0; k < 8; ++k)
+        v[k] = load_f64(T.rsrc, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, T.h - 1) * T.w * 8));
 #pragma unroll
-    for (int m2 = 0; m2 <= RAD; ++m2) {  // window column pairs 2m2, 2m2+1
-      if (m2 < RAD) {
+      for (int k = 0; k < 8; ++k)
 #pragma unroll
-        for (int m = 0; m < kVT / 2; ++m)
-          nxt[m] = *reinterpret_cast<const double2*>(base + 2 * m * T.VW + 2 * (m2 + 1));
-      }
-      const int i0 = 2 * m2, i1 = 2 * m2 + 1;
+        for (int t = 0; t < 8; ++t) acc[t] = fma((double)wp[jb + k - t], v[k], acc[t]);  // zero-padded taps
+    }
+    if (c < NC) {
+      double* dst = V + 8 * T.wv * T.sw + c;
 #pragma unroll
-      for (int m = 0; m < kVT / 2; ++m) {
-        const double2 v = cur[m];
-        out[2 * m] = fma((double)wp[i0], v.x, out[2 * m]);
-        if (i0 >= 1) out[2 * m + 1] = fma((double)wp[i0 - 1], v.x, out[2 * m + 1]);
-        if (i1 <= 2 * RAD) out[2 * m] = fma((double)wp[i1], v.y, out[2 * m]);
-        out[2 * m + 1] = fma((double)wp[i1 - 1], v.y, out[2 * m + 1]);
+      for (int t = 0; t < 8; ++t) dst[t * T.sw] = acc[t];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Vertical pass, octave 0, staged input region: input column kb + c (kb =
+// x0/2 - ceil(r/2)), output rows e + t (e = y0 + 8 wv, even).  Tap k of
+// output row e + t reads input row e/2 + floor((t + k - r)/2), i.e. window
+// row m = floor((t + k - r)/2) + ceil(r/2).
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void vert_o0(const GTile& T, const cdouble* wp, double* V) {
+  constexpr int HR = cl2(R);
+  constexpr int NC = fl2(kGX - 1 + R) + HR + 1;
+  constexpr int M = fl2(7 + R) + HR + 1;
+  static_assert(NC <= 64, "one lane per input column");
+  const int c = T.lane;
+  if (c < NC) {
+    const double* sp = T.S0 + (4 * T.wv + T.hrm - HR) * kBW0 + (c + T.hrm - HR);
+    double acc[8], v[M];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+#pragma unroll
+    for (int m = 0; m < kPFL && m < M; ++m) v[m] = sp[m * kBW0];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (m + kPFL < M) v[m + kPFL] = sp[(m + kPFL) * kBW0];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const int k = 2 * (m - HR) + R - t + d;
+          if (k >= 0 && k <= 2 * R) acc[t] = fma((double)wp[k], v[m], acc[t]);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int m = 0; m < kVT / 2; ++m) cur[m] = nxt[m];
     }
-  } else {
-#pragma unroll 1
-    for (int m2 = 0; m2 <= r; ++m2) {
-      const double w0 = wp[2 * m2], w1 = wp[2 * m2 + 1], wm = wp[2 * m2 - 1];  // zero-padded
+    double* dst = V + 8 * T.wv * T.sw + c;
 #pragma unroll
-      for (int m = 0; m < kVT / 2; ++m) {
-        const double2 v = *reinterpret_cast<const double2*>(base + 2 * m * T.VW + 2 * m2);
-        out[2 * m] = fma(w0, v.x, out[2 * m]);
-        out[2 * m + 1] = fma(wm, v.x, out[2 * m + 1]);
-        out[2 * m] = fma(w1, v.y, out[2 * m]);
-        out[2 * m + 1] = fma(w0, v.y, out[2 * m + 1]);
+    for (int t = 0; t < 8; ++t) dst[t * T.sw] = acc[t];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Horizontal pass: lane -> columns 4 cg .. 4 cg + 3, rows 8 wv + rs + 4 i.
+// o >= 1: out[q] = sum_k w_k V[row][4 cg + q + k].
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void horz_full(const GTile& T, const cdouble* wp, const double* V,
+                                          double (&out)[kNR][4]) {
+  constexpr int NP = R + 2;  // double2 pairs per row
+#pragma unroll
+  for (int i = 0; i < kNR; ++i) {
+    const double* rp = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 4 * T.cg;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    double2 u[NP];
+#pragma unroll
+    for (int n2 = 0; n2 < kPFH && n2 < NP; ++n2) u[n2] = *reinterpret_cast<const double2*>(rp + 2 * n2);
+#pragma unroll
+    for (int n2 = 0; n2 < NP; ++n2) {
+      if (n2 + kPFH < NP) u[n2 + kPFH] = *reinterpret_cast<const double2*>(rp + 2 * (n2 + kPFH));
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int n = 2 * n2 + e;
+        const double v = e ? u[n2].y : u[n2].x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = n - q;
+          if (k >= 0 && k <= 2 * R) a[q] = fma((double)wp[k], v, a[q]);
+        }
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[i][q] = a[q];
   }
 }
 
-template <bool OCT0, bool STAGED, int RAD>
-__device__ __forceinline__ void scale_step(const TileCtx& T, const cdouble* wp, int r, double (&out)[kVT]) {
-  vert_pass<OCT0, STAGED, RAD>(T, wp, r);
-  __syncthreads();
-  horz_pass<RAD>(T, wp, r, out);
-  __syncthreads();  // the strip is rewritten by the next scale
+__device__ __forceinline__ void horz_full_gen(const GTile& T, int r, const cdouble* wp, const double* V,
+                                              double (&out)[kNR][4]) {
+  const int NV = 2 * r + 4;
+#pragma unroll
+  for (int i = 0; i < kNR; ++i) {
+    const double* rp = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 4 * T.cg;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int nb = 0; nb < NV; nb += 8) {
+      double u[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const double2 p = *reinterpret_cast<const double2*>(rp + nb + 2 * e);
+        u[2 * e] = p.x;
+        u[2 * e + 1] = p.y;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = fma((double)wp[nb + e - q], u[e], a[q]);  // zero-padded taps
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[i][q] = a[q];
+  }
 }
 
-template <bool OCT0, bool STAGED, int... Rs>
-__device__ __forceinline__ void dispatch_scale(std::integer_sequence<int, Rs...>, const TileCtx& T,
-                                               const cdouble* wp, int r, double (&out)[kVT]) {
+// Octave 0: strip column n <-> input column x0/2 - ceil(r/2) + n; tap k of
+// output column x0 + 4 cg + q reads strip column 2 cg + floor((q + k - r)/2) + ceil(r/2).
+template <int R>
+__device__ __forceinline__ void horz_o0(const GTile& T, const cdouble* wp, const double* V,
+                                        double (&out)[kNR][4]) {
+  constexpr int HR = cl2(R);
+  constexpr int NP = (fl2(R + 3) + HR + 2) / 2;  // double2 pairs per row
+#pragma unroll
+  for (int i = 0; i < kNR; ++i) {
+    const double* rp = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 2 * T.cg;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    double2 u[NP];
+#pragma unroll
+    for (int n2 = 0; n2 < kPFH && n2 < NP; ++n2) u[n2] = *reinterpret_cast<const double2*>(rp + 2 * n2);
+#pragma unroll
+    for (int n2 = 0; n2 < NP; ++n2) {
+      if (n2 + kPFH < NP) u[n2 + kPFH] = *reinterpret_cast<const double2*>(rp + 2 * (n2 + kPFH));
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int n = 2 * n2 + e;
+        const double v = e ? u[n2].y : u[n2].x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const int k = 2 * (n - HR) + R - q + d;
+            if (k >= 0 && k <= 2 * R) a[q] = fma((double)wp[k], v, a[q]);
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[i][q] = a[q];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Radius dispatch (uniform branch).
+// ---------------------------------------------------------------------------
+template <bool OCT0, int... Rs>
+__device__ __forceinline__ void vert_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
+                                         const cdouble* wp, double* V) {
   bool done = false;
-  ((!done && r == Rs ? (scale_step<OCT0, STAGED, Rs>(T, wp, r, out), done = true) : false), ...);
-  if (!done) scale_step<OCT0, STAGED, -1>(T, wp, r, out);
-}
-
-// Staged base region of a tile (rows rlo..rhi, BW columns): octave 0 stages
-// input pixels (rows q = y>>1, columns k = x>>1); octave o>=1 the fp64 seed.
-struct Region {
-  int rlo, rhi, BW, kb_all;
-};
-
-__host__ __device__ inline Region tile_region(const Pyramid& P, int o, int x0, int y0) {
-  const Octave& oc = P.oct[o];
-  const int R = oc.rmax;
-  Region g;
-  if (o == 0) {
-    g.rlo = max(0, (y0 - R) >> 1);
-    g.rhi = min(P.H - 1, (y0 + kTY - 1 + R) >> 1);
-    g.kb_all = (x0 - R) >> 1;
-    g.BW = ((x0 + kTX - 1 + R) >> 1) - g.kb_all + 1;
+  if constexpr (OCT0) {
+    ((!done && r == Rs ? (vert_o0<Rs>(T, wp, V), done = true) : false), ...);
   } else {
-    g.rlo = max(0, y0 - R);
-    g.rhi = min(oc.h - 1, y0 + kTY - 1 + R);
-    g.kb_all = 0;
-    g.BW = kTX + 2 * R;
+    ((!done && r == Rs ? (vert_glob<Rs>(T, wp, V), done = true) : false), ...);
+    if (!done) vert_glob_gen(T, r, wp, V);
   }
-  return g;
 }
 
-template <bool OCT0, bool STAGED>
+template <bool OCT0, int... Rs>
+__device__ __forceinline__ void horz_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
+                                         const cdouble* wp, const double* V, double (&out)[kNR][4]) {
+  bool done = false;
+  if constexpr (OCT0) {
+    ((!done && r == Rs ? (horz_o0<Rs>(T, wp, V, out), done = true) : false), ...);
+  } else {
+    ((!done && r == Rs ? (horz_full<Rs>(T, wp, V, out), done = true) : false), ...);
+    if (!done) horz_full_gen(T, r, wp, V, out);
+  }
+}
+
+// Unrolled radii 0..RMAX.
+template <bool OCT0, int RMAX>
+__device__ __forceinline__ void vert_any(const GTile& T, int r, const cdouble* wp, double* V) {
+  vert_any_<OCT0>(std::make_integer_sequence<int, RMAX + 1>{}, T, r, wp, V);
+}
+template <bool OCT0, int RMAX>
+__device__ __forceinline__ void horz_any(const GTile& T, int r, const cdouble* wp, const double* V,
+                                         double (&out)[kNR][4]) {
+  horz_any_<OCT0>(std::make_integer_sequence<int, RMAX + 1>{}, T, r, wp, V, out);
+}
+
+__device__ __forceinline__ void store4(float* p, const double (&v)[4], int nvalid) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < nvalid) p[q] = (float)v[q];
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte buffer store; lanes whose offset is past the plane are dropped by
+// the descriptor's range check.
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t rs, int voff, const double (&v)[4]) {
+  const float4 f = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), rs, voff, 0, 0);
+}
+
+// SWC > 0: compile-time strip stride (immediate LDS offsets); 0: L.sw.
+// RMAX: radii with unrolled code.
+template <bool OCT0, int SWC, int RMAX>
 __global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  TileCtx T;
-  T.P = &P;
-  T.oc = &P.oct[L.o];
-  T.h = T.oc->h;
-  T.w = T.oc->w;
-  T.R = T.oc->rmax;
-  T.VW = kTX + 2 * T.R + 2;  // even: 16-byte aligned column pairs
-  T.x0 = blockIdx.x * kTX;
-  T.y0 = blockIdx.y * kTY;
+  const Octave& oc = P.oct[L.o];
+  GTile T;
+  T.h = oc.h;
+  T.w = oc.w;
+  T.x0 = blockIdx.x * kGX;
+  T.y0 = blockIdx.y * kGY;
   T.lane = threadIdx.x & 63;
-  T.wv = threadIdx.x >> 6;
-  T.sV = smem;
-  T.sB = nullptr;
-  T.rlo = 0;
-  T.BW = 0;
-  T.kb_all = 0;
-  const int h = T.h, w = T.w;
-  if (STAGED) {
-    const Region g = tile_region(P, L.o, T.x0, T.y0);
-    T.rlo = g.rlo;
-    T.BW = g.BW;
-    T.kb_all = g.kb_all;
-    T.sB = smem + kTY * T.VW;
-    // Row segments per wave, 4 rows per batch: all loads of a batch are in
-    // flight before the first LDS store (no per-element latency chain).
-    const int nr = g.rhi - g.rlo + 1;
-    for (int rb = T.wv * 4; rb < nr; rb += 16) {
-      for (int cc = T.lane; cc < g.BW; cc += 64) {
-        double v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int rr = min(rb + k, nr - 1);
-          if (OCT0) v[k] = (double)P.img[(long long)(g.rlo + rr) * P.img_stride + clampi(g.kb_all + cc, 0, P.W - 1)];
-          else v[k] = P.seeds[T.oc->seed_off + (long long)(g.rlo + rr) * w + clampi(T.x0 - T.R + cc, 0, w - 1)];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (rb + k < nr) T.sB[(rb + k) * g.BW + cc] = v[k];
-      }
+  T.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  T.cg = T.lane & (kCG - 1);
+  T.rs = T.lane / kCG;
+  T.sw = SWC > 0 ? SWC : L.sw;
+  T.hrm = cl2(oc.rmax);
+  if (!OCT0)
+    T.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L.base), 0, T.h * T.w * 8, 0x00020000);
+  const int nstrip = (L.db ? 2 : 1) * kGY * T.sw;
+  T.S0 = smem + nstrip;
+  double* V0 = smem;
+  double* V1 = L.db ? smem + kGY * T.sw : smem;
+
+  // The generic horizontal path reads (with zero taps) past the columns a
+  // scale writes: those must be finite.
+  if (L.zero)
+    for (int i = threadIdx.x; i < nstrip; i += 256) smem[i] = 0.0;
+  if (OCT0) {
+    // Stage input rows y0/2 - hrm .. and columns x0/2 - hrm .. as fp64,
+    // clamped (replicate edges): the region every scale's windows read.
+    const int q0 = T.y0 / 2 - T.hrm, k0 = T.x0 / 2 - T.hrm;
+    const int nr = fl2(kGY - 1 + oc.rmax) + T.hrm + 1;
+    const int nc = fl2(kGX - 1 + oc.rmax) + T.hrm + 1;
+    double* S0 = smem + nstrip;
+    const int kk = clampi(k0 + T.lane, 0, P.W - 1);
+    for (int rr = T.wv; rr < nr; rr += 4) {
+      const float* src = P.img + (long long)clampi(q0 + rr, 0, P.H - 1) * P.img_stride;
+      if (T.lane < nc) S0[rr * kBW0 + T.lane] = (double)src[kk];
     }
-    __syncthreads();
   }
-  const long long plane = (long long)h * w;
-  const int p = T.lane & 31, half = T.lane >> 5;
-  const int x = T.x0 + 2 * p;
-  double lprev[kVT];
+  const long long plane = (long long)T.h * T.w;
+  const int x = T.x0 + 4 * T.cg;
+  const int nvalid = T.w - x;
+  // Per-lane byte offsets of its two output rows in a plane (past the plane:
+  // the store is dropped).
+  int voff[kNR];
 #pragma unroll
-  for (int q = 0; q < kVT; ++q) lprev[q] = 0.0;
+  for (int i = 0; i < kNR; ++i) {
+    const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
+    voff[i] = (y < T.h && nvalid > 0) ? (y * T.w + x) * 4 : 0x7ffffff0;
+  }
 
   // Scale group of this block (small octaves split their scales over
   // blockIdx.z for parallelism; a group recomputes the scale before it as
   // the DoG's L_{s-1}, without storing it).
   const int G = gridDim.z, per = (P.NS + G - 1) / G;
   const int s_begin = blockIdx.z * per, s_end = min(P.NS, s_begin + per);
-  for (int s = max(0, s_begin - 1); s < s_end; ++s) {
-    const bool store = s >= s_begin;
-    const int r = T.oc->rad[s];
-    // Taps through the constant address space: wave-uniform scalar loads.
-    const cdouble* wp = (const cdouble*)(P.wts + T.oc->wofs[s]);
-    double out[kVT];
-    dispatch_scale<OCT0, STAGED>(std::make_integer_sequence<int, kRT + 1>{}, T, wp, r, out);
+  const int s_first = max(0, s_begin - 1);
+  __syncthreads();
+  vert_any<OCT0, RMAX>(T, oc.rad[s_first], (const cdouble*)(P.wts + oc.wofs[s_first]), V0);
+  __syncthreads();
 
+  const bool st = !(L.dbg & 1);  // dbg 1: timing without plane stores
+  double lprev[kNR][4];
+  for (int s = s_first; s < s_end; ++s) {
+    const int ph = (s - s_first) & 1;
+    const double* cur = ph ? V1 : V0;
+    double* nxt = ph ? V0 : V1;
+    double out[kNR][4];
+    horz_any<OCT0, RMAX>(T, oc.rad[s], (const cdouble*)(P.wts + oc.wofs[s]), cur, out);
+
+    if (s >= s_begin && (st || out[0][0] == 12345.0)) {
+      double d[kNR][4];
 #pragma unroll
-    for (int m = 0; m < kVT / 2; ++m) {
-      const int y = T.y0 + T.wv * kVT + 2 * m + half;
-      if (store && y < h && x < w) {
-        const long long pp = (long long)y * w + x;
-        const double a = out[2 * m], b = out[2 * m + 1];
-        const bool has_b = x + 1 < w;
+      for (int i = 0; i < kNR; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
+      if (L.vec) {
+        const unsigned pb = (unsigned)plane * 4u;
         if (L.gauss) {
-          float* g = L.gauss + s * plane + pp;
-          if (has_b && !(((long long)s * plane + pp) & 1)) {  // float2 needs 8-byte alignment
-            *reinterpret_cast<float2*>(g) = make_float2((float)a, (float)b);
-          } else {
-            g[0] = (float)a;
-            if (has_b) g[1] = (float)b;
+          const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L.gauss + s * plane, 0, pb, 0x00020000);
+#pragma unroll
+          for (int i = 0; i < kNR; ++i) bstore4(rg, voff[i], out[i]);
+        }
+        if (s > 0) {
+          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L.dog + (s - 1) * plane, 0, pb, 0x00020000);
+#pragma unroll
+          for (int i = 0; i < kNR; ++i) bstore4(rd, voff[i], d[i]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kNR; ++i) {
+          const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
+          if (y < T.h && nvalid > 0) {
+            const long long pp = (long long)y * T.w + x;
+            if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
+            if (s > 0) store4(L.dog + (s - 1) * plane + pp, d[i], nvalid);
           }
         }
-        if (s > 0) {  // lprev = L_{s-1}: computed here even when s-1 belongs to the previous group
-          float* d = L.dog + (s - 1) * plane + pp;
-          const float da = (float)(lprev[2 * m] - a), db = (float)(lprev[2 * m + 1] - b);
-          if (has_b && !(((long long)(s - 1) * plane + pp) & 1)) {
-            *reinterpret_cast<float2*>(d) = make_float2(da, db);
-          } else {
-            d[0] = da;
-            if (has_b) d[1] = db;
-          }
+      }
+    }
+    if (s == P.S && L.next_seed && s >= s_begin) {
+#pragma unroll
+      for (int i = 0; i < kNR; ++i) {
+        const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
+        if (y < T.h && nvalid > 0 && !(y & 1)) {
+          double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+          sd[0] = out[i][0];
+          if (nvalid > 2) sd[1] = out[i][2];
         }
-        if (s == P.S && L.next_seed && !(y & 1))
-          L.next_seed[(long long)(y >> 1) * L.next_w + (x >> 1)] = a;
       }
     }
 #pragma unroll
-    for (int q = 0; q < kVT; ++q) lprev[q] = out[q];
+    for (int i = 0; i < kNR; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
+    // The next scale's vertical pass, after this scale's stores: its
+    // registers do not overlap the epilogue's.
+    if (!L.db) __syncthreads();
+    if (s + 1 < s_end)
+      vert_any<OCT0, RMAX>(T, oc.rad[s + 1], (const cdouble*)(P.wts + oc.wofs[s + 1]), nxt);
+    __syncthreads();
+  }
+}
+
+// Materialised octave-0 base (fp64), for octave-0 radii beyond kUR.
+__global__ __launch_bounds__(256) void k_upsample_base(const Pyramid P, double* __restrict__ b) {
+  const int h = P.oct[0].h, w = P.oct[0].w;
+  const long long n = (long long)h * w;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int y = (int)(i / w), x = (int)(i - (long long)y * w);
+    b[i] = (double)P.img[(long long)min(y >> 1, P.H - 1) * P.img_stride + min(x >> 1, P.W - 1)];
   }
 }
 
@@ -324,61 +482,79 @@ __global__ __launch_bounds__(256) void k_dog_from_gauss(const float* __restrict_
   }
 }
 
-static size_t strip_bytes(const Octave& oc) { return sizeof(double) * (size_t)kTY * (kTX + 2 * oc.rmax + 2); }
+bool gauss_needs_base0(const Pyramid& P) { return P.oct[0].rmax > kUR; }
 
-static size_t region_bytes(const Pyramid& P, int o) {
-  const Octave& oc = P.oct[o];
-  const int R = oc.rmax;
-  if (o == 0) return sizeof(double) * (size_t)std::min(P.H, (kTY + 2 * R) / 2 + 2) * ((kTX + 2 * R) / 2 + 2);
-  return sizeof(double) * (size_t)std::min(oc.h, kTY + 2 * R) * (kTX + 2 * R);
+static bool staged0(const Pyramid& P, int o) { return o == 0 && !gauss_needs_base0(P); }
+
+// Strip row stride: covers the widest read of the horizontal pass (generic
+// path: 4 (kCG - 1) + round_up(2r + 4, 8)).
+constexpr int kSW0 = 2 * (kCG - 1) + 8 + 6;   // octave-0 strip stride for rmax <= 8
+constexpr int kSW1 = 2 * (kCG - 1) + kUR + 6;  // ... rmax <= kUR
+
+static int strip_stride(const Pyramid& P, int o) {
+  const int R = P.oct[o].rmax;
+  if (staged0(P, o)) return R <= 8 ? kSW0 : kSW1;
+  return kGX + 2 * R + 12;
 }
 
-// Octave 0 stages its (tiny) input region; octaves o >= 1 read the fp64 seed
-// through L1/L2, which keeps the LDS per block small and occupancy high.
-// SIFT_STAGE_OCTAVES (bit mask, default 1) overrides for A/B measurements.
-static bool staged(const Pyramid& P, int o) {
-  static const int mask = [] {
-    const char* e = std::getenv("SIFT_STAGE_OCTAVES");
-    return e ? std::atoi(e) : 1;
-  }();
-  return ((mask >> o) & 1) && strip_bytes(P.oct[o]) + region_bytes(P, o) <= 96 * 1024;
+static size_t staged_bytes(const Pyramid& P, int o) {
+  if (!staged0(P, o)) return 0;
+  const int R = P.oct[0].rmax;
+  return sizeof(double) * (size_t)(fl2(kGY - 1 + R) + cl2(R) + 1) * kBW0;
+}
+
+static bool double_buffer(const Pyramid& P, int o) {
+  return sizeof(double) * 2 * kGY * strip_stride(P, o) + staged_bytes(P, o) <= 64 * 1024;
+}
+
+size_t gauss_lds_bytes(const Pyramid& P, int o) {
+  return sizeof(double) * (double_buffer(P, o) ? 2 : 1) * kGY * strip_stride(P, o) + staged_bytes(P, o);
 }
 
 // Scale groups per octave: enough blocks to fill 256 CUs several times.
 static int scale_groups(const Pyramid& P, int o) {
   const Octave& oc = P.oct[o];
-  const long long tiles = (long long)((oc.w + kTX - 1) / kTX) * ((oc.h + kTY - 1) / kTY);
+  const long long tiles = (long long)((oc.w + kGX - 1) / kGX) * ((oc.h + kGY - 1) / kGY);
   int g = 1;
   while (g < P.NS / 2 && tiles * g < 2048) g *= 2;
   return g;
 }
 
-size_t gauss_lds_bytes(const Pyramid& P, int o) {
-  return strip_bytes(P.oct[o]) + (staged(P, o) ? region_bytes(P, o) : 0);
-}
-
-template <bool O0, bool ST>
+template <bool O0, int SWC, int RMAX>
 static void set_attr() {
-  (void)hipFuncSetAttribute((const void*)k_gauss_dog<O0, ST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_gauss_dog<O0, SWC, RMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
 }
 
-hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t st) {
+hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st) {
+  const long long n = (long long)P.oct[0].h * P.oct[0].w;
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_upsample_base, dim3(blocks), dim3(256), 0, st, P, base0);
+  return hipGetLastError();
+}
+
+hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
   const Octave& oc = P.oct[L.o];
-  dim3 grid((oc.w + kTX - 1) / kTX, (oc.h + kTY - 1) / kTY, scale_groups(P, L.o));
+  dim3 grid((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, scale_groups(P, L.o));
   const size_t lds = gauss_lds_bytes(P, L.o);
   static bool attr_set = false;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    set_attr<true, true>();
-    set_attr<true, false>();
-    set_attr<false, true>();
-    set_attr<false, false>();
+    set_attr<true, kSW0, 8>();
+    set_attr<true, kSW1, kUR>();
+    set_attr<false, 0, kUR>();
     attr_set = true;
   }
-  const bool o0 = L.o == 0, stg = staged(P, L.o);
-  if (o0 && stg) hipLaunchKernelGGL((k_gauss_dog<true, true>), grid, dim3(256), lds, st, P, L);
-  else if (o0) hipLaunchKernelGGL((k_gauss_dog<true, false>), grid, dim3(256), lds, st, P, L);
-  else if (stg) hipLaunchKernelGGL((k_gauss_dog<false, true>), grid, dim3(256), lds, st, P, L);
-  else hipLaunchKernelGGL((k_gauss_dog<false, false>), grid, dim3(256), lds, st, P, L);
+  L.sw = strip_stride(P, L.o);
+  L.db = double_buffer(P, L.o) ? 1 : 0;
+  static const int dbg = [] { const char* e = std::getenv("SIFT_GAUSS_DBG"); return e ? std::atoi(e) : 0; }();
+  L.dbg = dbg;
+  const bool a16 = !((reinterpret_cast<uintptr_t>(L.dog)) & 15) &&
+                   (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
+  L.vec = (a16 && (oc.w & 3) == 0 && 4.0 * oc.h * oc.w < 2147483648.0) ? 1 : 0;
+  L.zero = oc.rmax > kUR ? 1 : 0;
+  if (staged0(P, L.o) && L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8>), grid, dim3(256), lds, st, P, L);
+  else if (staged0(P, L.o)) hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR>), grid, dim3(256), lds, st, P, L);
+  else hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR>), grid, dim3(256), lds, st, P, L);
   return hipGetLastError();
 }
 

@@ -18,6 +18,13 @@ struct GaussLaunch {
   float* dog;         // plane (o, 0) of the DoG pyramid
   double* next_seed;  // base of octave o+1 (nullptr for the last octave)
   int next_w;
+  const double* base; // fp64 octave base h x w (o >= 1: the seed; o == 0: only when materialised)
+  // filled by launch_gauss_dog
+  int sw;             // strip row stride (doubles)
+  int db;             // double-buffered strips
+  int vec;            // float4 plane stores are aligned
+  int zero;           // strips need zeroing (generic-radius path present)
+  int dbg;            // timing experiments (SIFT_GAUSS_DBG): bit 0 = no plane stores
 };
 
 constexpr int kXW = 62;      // output columns per extrema wave (lanes 1..62; lanes 0, 63 are halo)
@@ -81,7 +88,11 @@ struct RefineLaunch {
 };
 
 size_t gauss_lds_bytes(const Pyramid& P, int o);
-hipError_t launch_gauss_dog(const Pyramid& P, const GaussLaunch& L, hipStream_t st);
+// Octave 0 radii above the unrolled range run on a materialised fp64 upsample
+// of the input (4 H W doubles) instead of the staged input region.
+bool gauss_needs_base0(const Pyramid& P);
+hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st);
+hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st);
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
 
 // Fills the unit table of L (octave geometry) and launches the scan; returns
