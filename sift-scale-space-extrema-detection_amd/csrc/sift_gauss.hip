@@ -7,23 +7,26 @@
 // The reference convolves every scale of an octave with a full 2D kernel of
 // the SAME octave base (the blur is not incremental, background.js:173-177).
 // The 2D kernel is exactly separable (w(i) w(j), sift.js:22-67).  One block
-// owns a 64x32 output tile and walks all scales of the octave over it:
+// owns a 64x32 output tile; each of its 4 waves owns 8 rows of it and walks
+// all scales of the octave on its own (no block barrier after the staging):
 //
-//   vertical pass   base -> fp64 LDS strip V[32][...]: one lane per column,
-//                   an 8-row register window per wave (8 accumulators, every
-//                   base value loaded once per window);
+//   vertical pass   base -> fp64 LDS strip rows 8 wv .. 8 wv + 7, columns
+//                   x0 - r .. x0 + 63 + r: lanes are columns with an 8-row
+//                   register window (every base value loaded once per
+//                   window); the 2r halo columns are packed into one pass of
+//                   (column, row-slice) lanes;
 //   horizontal pass strip -> 4 adjacent columns x 2 rows per lane, the row
 //                   window read with 16-byte LDS loads;
 //   epilogue        L_s and DoG L_{s-1} - L_s (formed in fp64, rounded once)
-//                   as float4 stores; for s == S the fp64 seed of the next
-//                   octave (background.js:114-118).
+//                   as 16-byte buffer stores; for s == S the fp64 seed of the
+//                   next octave (background.js:114-118).
 //
-// The strips are double-buffered: the vertical pass of scale s+1 runs
-// between the horizontal pass and the stores of scale s, one barrier per
-// scale.  Radii 0..kUR run fully unrolled code specialised on the radius
-// (every tap an SGPR operand of v_fma_f64, every load an immediate-offset
-// LDS read or a scalar-row global read); larger radii run 8-wide chunks over
-// zero-padded taps (fma(0, v, acc) == acc, so the results are identical).
+// A wave touches only its own strip rows, so the only ordering it needs is
+// its own (wave_lds_fence).  Radii 0..RMAX run fully unrolled code
+// specialised on the radius (every tap an SGPR operand of v_fma_f64, every
+// load an immediate-offset LDS read or a buffer load with the row in an
+// SGPR); larger radii run 8-wide chunks over zero-padded taps (fma(0, v, acc)
+// == acc, so the results are identical).
 //
 // Octave 0's base is the 2x nearest-neighbour upsample of the input
 // (background.js:84): B[y][x] = I[clamp(y>>1)][clamp(x>>1)], never
@@ -38,8 +41,9 @@
 // the result is translation invariant like the reference's 2D sum, and
 // sift_exact.h reproduces any single pixel bit for bit.
 //
-// Roofline: HBM-bound on the plane stores: per octave pixel 4(S+3) + 4(S+2)
-// bytes written against 1 (octave 0) or 8 bytes of base read.
+// Roofline: octave 0 is HBM-bound on the plane stores (per octave pixel
+// 4(S+3) + 4(S+2) bytes written against 1 byte of input read); the small
+// octaves, whose radii double per octave, are bound by fp64 FMA issue.
 #include <cstdlib>
 #include <utility>
 
@@ -50,12 +54,22 @@ namespace sift {
 
 constexpr int kGX = 64;              // tile columns
 constexpr int kGY = 32;              // tile rows: 4 waves x 8
-constexpr int kUR = 16;              // radii with unrolled code
+constexpr int kUR = 16;              // radii with unrolled code (octave 0)
+#ifndef SIFT_UR1
+#define SIFT_UR1 8
+#endif
+#ifndef SIFT_STORE_AUX
+#define SIFT_STORE_AUX 18 // cache-policy bits of the plane stores (gfx950: 1 sc0, 2 nt, 16 sc1)
+#endif
+#ifndef SIFT_MINW1
+#define SIFT_MINW1 1
+#endif
+constexpr int kUR1 = SIFT_UR1;       // ... octaves >= 1 (SGPR budget: taps are SGPR operands)
 constexpr int kCG = kGX / 4;         // column groups of 4 outputs (16)
 constexpr int kRS = 64 / kCG;        // row sub-groups per wave (4)
 constexpr int kNR = 8 / kRS;         // rows per lane in the horizontal pass (2)
 constexpr int kBW0 = kGX / 2 + kUR + 4;  // staged octave-0 region width (input columns)
-constexpr int kPFV = 6;              // rows in flight, vertical pass from global memory
+constexpr int kPFV = 12;             // rows in flight, vertical pass from global memory
 constexpr int kPFL = 4;              // rows in flight, vertical pass from LDS
 constexpr int kPFH = 3;              // 16-byte reads in flight, horizontal pass
 
@@ -72,49 +86,112 @@ struct GTile {
   __amdgpu_buffer_rsrc_t rsrc;  // o >= 1 (or materialised octave 0): fp64 base plane h x w
 };
 
+// Register pinning: an empty asm that reads and writes the accumulators and
+// clobbers memory.  The compiler keeps the source order of the fma chains
+// and cannot hoist later loads above it, so the register window stays the
+// size written (the scheduling-barrier builtin does not stop the selection
+// DAG from delaying whole fma chains and keeping every loaded value alive).
+template <int N>
+__device__ __forceinline__ void pin(double (&a)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i])::"memory");
+}
+
+// LDS hand-off between the lanes of ONE wave: the wave's LDS operations
+// execute in order, so waiting for its own outstanding ones (and keeping the
+// compiler from moving LDS accesses across) is all the ordering needed.
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ double load_f64(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
 }
 
 // ---------------------------------------------------------------------------
-// Vertical pass, base plane in global memory (L1/L2): V[8 wv + t][c] =
-// sum_k w_k B[y0 + 8 wv + t - r + k][x0 - r + c], c in [0, 64 + 2r).
+// Vertical window: acc[t] = sum_k w_k row_{t+k} (t < NO, k <= 2R) over the
+// rows ld() returns in order, kPFV loads in flight.
+// ---------------------------------------------------------------------------
+template <int R, int NO, class Ld>
+__device__ __forceinline__ void vwin(const cdouble* wp, Ld&& ld, double (&acc)[NO]) {
+  constexpr int NJ = 2 * R + NO;
+  constexpr int PF = NJ < kPFV ? NJ : kPFV;
+  double v[NJ];
+#pragma unroll
+  for (int t = 0; t < NO; ++t) acc[t] = 0.0;
+#pragma unroll
+  for (int j = 0; j < PF; ++j) v[j] = ld();
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (j + PF < NJ) v[j + PF] = ld();
+#pragma unroll
+    for (int t = 0; t < NO; ++t) {
+      const int k = j - t;
+      if (k >= 0 && k <= 2 * R) acc[t] = fma((double)wp[k], v[j], acc[t]);
+    }
+    pin(acc);  // program order: loads and fma chains stay in their iteration
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Vertical pass, base plane in global memory (L1/L2), this wave's rows:
+// V[8 wv + t][c] = sum_k w_k B[y0 + 8 wv + t - R + k][x0 - R + c],
+// c in [0, 64 + 2R).  Pass A: columns 0..63, one lane each, 8 rows.  Pass B:
+// the 2R halo columns, lane -> (column 64 + l % 2R, row slice l / 2R of RB
+// rows), so few lanes idle.
 // ---------------------------------------------------------------------------
 template <int R>
 __device__ __forceinline__ void vert_glob(const GTile& T, const cdouble* wp, double* V) {
-  constexpr int NC = kGX + 2 * R;
-  constexpr int NJ = 2 * R + 8;
   const int yb = __builtin_amdgcn_readfirstlane(T.y0 + 8 * T.wv - R);
+  const int w8 = T.w * 8;
+  double* Vw = V + 8 * T.wv * T.sw;
+  {
+    const int xoff = clampi(T.x0 - R + T.lane, 0, T.w - 1) * 8;
+    // Row offsets from a loop-carried SGPR counter (opaque to the compiler,
+    // so it cannot precompute one SGPR per row of the window).
+    int yy = yb;
+    auto ld = [&]() -> double {
+      const double v = load_f64(T.rsrc, xoff, clampi(yy, 0, T.h - 1) * w8);
+      asm volatile("" : "+s"(yy));
+      yy += 1;
+      return v;
+    };
+    double acc[8];
+    vwin<R, 8>(wp, ld, acc);
 #pragma unroll
-  for (int cb = 0; cb < NC; cb += 64) {
-    const int c = cb + T.lane;
-    if (cb + 64 <= NC || c < NC) {
-      // Buffer loads: the column is a per-lane byte offset, the row a
-      // wave-uniform SGPR offset (no per-row address arithmetic in VGPRs).
-      const int xoff = clampi(T.x0 - R + c, 0, T.w - 1) * 8;
-      auto ld = [&](int j) -> double {
-        int yy = yb + j;
-        asm volatile("" : "+s"(yy));  // computed at its use: no early SGPR offsets for every row
-        return load_f64(T.rsrc, xoff, clampi(yy, 0, T.h - 1) * T.w * 8);
-      };
-      double acc[8], v[NJ];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = 0.0;
-#pragma unroll
-      for (int j = 0; j < kPFV && j < NJ; ++j) v[j] = ld(j);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        if (j + kPFV < NJ) v[j + kPFV] = ld(j + kPFV);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int k = j - t;
-          if (k >= 0 && k <= 2 * R) acc[t] = fma((double)wp[k], v[j], acc[t]);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // keep the window short (no hoisting of every load)
+    for (int t = 0; t < 8; ++t) Vw[t * T.sw + T.lane] = acc[t];
+  }
+  if constexpr (R > 0) {
+    constexpr int NB = 2 * R;
+    static_assert(NB <= 64, "halo columns fit one packed pass");
+    constexpr int G = 64 / NB;              // row slices side by side
+    constexpr int RB = (8 + G - 1) / G;     // rows per slice
+    constexpr int NSL = (8 + RB - 1) / RB;  // slices in use
+    const int col = T.lane % NB, sl = T.lane / NB;
+    if (sl < NSL) {
+      const int lr = sl * RB;
+      const int xoff = clampi(T.x0 - R + kGX + col, 0, T.w - 1) * 8;
+      double acc[RB];
+      if (yb >= 0 && yb + NSL * RB - 1 + 2 * R <= T.h - 1) {  // interior: no row clamping
+        const int vo = xoff + lr * w8;
+        int yy = yb;
+        auto ld = [&]() -> double {
+          const double v = load_f64(T.rsrc, vo, yy * w8);
+          asm volatile("" : "+s"(yy));
+          yy += 1;
+          return v;
+        };
+        vwin<R, RB>(wp, ld, acc);
+      } else {
+        int yy = yb + lr;
+        auto ld = [&]() -> double {
+          const double v = load_f64(T.rsrc, xoff + clampi(yy, 0, T.h - 1) * w8, 0);
+          yy += 1;
+          return v;
+        };
+        vwin<R, RB>(wp, ld, acc);
       }
-      double* dst = V + 8 * T.wv * T.sw + c;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) dst[t * T.sw] = acc[t];
+      for (int t = 0; t < RB; ++t)
+        if (lr + t < 8) Vw[(lr + t) * T.sw + kGX + col] = acc[t];
     }
   }
 }
@@ -137,6 +214,7 @@ __device__ __forceinline__ void vert_glob_gen(const GTile& T, int r, const cdoub
       for (int k = 0; k < 8; ++k)
 #pragma unroll
         for (int t = 0; t < 8; ++t) acc[t] = fma((double)wp[jb + k - t], v[k], acc[t]);  // zero-padded taps
+      pin(acc);
     }
     if (c < NC) {
       double* dst = V + 8 * T.wv * T.sw + c;
@@ -177,7 +255,7 @@ __device__ __forceinline__ void vert_o0(const GTile& T, const cdouble* wp, doubl
           if (k >= 0 && k <= 2 * R) acc[t] = fma((double)wp[k], v[m], acc[t]);
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
+      pin(acc);
     }
     double* dst = V + 8 * T.wv * T.sw + c;
 #pragma unroll
@@ -213,7 +291,7 @@ __device__ __forceinline__ void horz_full(const GTile& T, const cdouble* wp, con
           if (k >= 0 && k <= 2 * R) a[q] = fma((double)wp[k], v, a[q]);
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
+      pin(a);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) out[i][q] = a[q];
@@ -239,6 +317,7 @@ __device__ __forceinline__ void horz_full_gen(const GTile& T, int r, const cdoub
       for (int e = 0; e < 8; ++e)
 #pragma unroll
         for (int q = 0; q < 4; ++q) a[q] = fma((double)wp[nb + e - q], u[e], a[q]);  // zero-padded taps
+      pin(a);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) out[i][q] = a[q];
@@ -275,7 +354,7 @@ __device__ __forceinline__ void horz_o0(const GTile& T, const cdouble* wp, const
           }
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
+      pin(a);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) out[i][q] = a[q];
@@ -332,20 +411,21 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // the descriptor's range check.
 __device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t rs, int voff, const double (&v)[4]) {
   const float4 f = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), rs, voff, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), rs, voff, 0, SIFT_STORE_AUX);
 }
 
 // SWC > 0: compile-time strip stride (immediate LDS offsets); 0: L.sw.
 // RMAX: radii with unrolled code.
 template <bool OCT0, int SWC, int RMAX>
-__global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
+__global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const Octave& oc = P.oct[L.o];
+  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   GTile T;
   T.h = oc.h;
   T.w = oc.w;
-  T.x0 = blockIdx.x * kGX;
-  T.y0 = blockIdx.y * kGY;
+  T.x0 = bx * kGX;
+  T.y0 = by * kGY;
   T.lane = threadIdx.x & 63;
   T.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   T.cg = T.lane & (kCG - 1);
@@ -354,10 +434,11 @@ __global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussL
   T.hrm = cl2(oc.rmax);
   if (!OCT0)
     T.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L.base), 0, T.h * T.w * 8, 0x00020000);
-  const int nstrip = (L.db ? 2 : 1) * kGY * T.sw;
+  // One strip: every wave writes (vertical pass) and reads (horizontal pass)
+  // only its own 8 strip rows.
+  const int nstrip = kGY * T.sw;
   T.S0 = smem + nstrip;
-  double* V0 = smem;
-  double* V1 = L.db ? smem + kGY * T.sw : smem;
+  double* V = smem;
 
   // The generic horizontal path reads (with zero taps) past the columns a
   // scale writes: those must be finite.
@@ -392,20 +473,19 @@ __global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussL
   // blockIdx.z for parallelism; a group recomputes the scale before it as
   // the DoG's L_{s-1}, without storing it).
   const int G = gridDim.z, per = (P.NS + G - 1) / G;
-  const int s_begin = blockIdx.z * per, s_end = min(P.NS, s_begin + per);
+  const int s_begin = bz * per, s_end = min(P.NS, s_begin + per);
   const int s_first = max(0, s_begin - 1);
-  __syncthreads();
-  vert_any<OCT0, RMAX>(T, oc.rad[s_first], (const cdouble*)(P.wts + oc.wofs[s_first]), V0);
-  __syncthreads();
+  __syncthreads();  // staged region / zeroed strip visible to every wave
 
   const bool st = !(L.dbg & 1);  // dbg 1: timing without plane stores
   double lprev[kNR][4];
   for (int s = s_first; s < s_end; ++s) {
-    const int ph = (s - s_first) & 1;
-    const double* cur = ph ? V1 : V0;
-    double* nxt = ph ? V0 : V1;
+    const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+    vert_any<OCT0, RMAX>(T, oc.rad[s], wp, V);
+    wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
     double out[kNR][4];
-    horz_any<OCT0, RMAX>(T, oc.rad[s], (const cdouble*)(P.wts + oc.wofs[s]), cur, out);
+    horz_any<OCT0, RMAX>(T, oc.rad[s], wp, V, out);
+    wave_lds_fence();  // strip rows read before the next scale overwrites them
 
     if (s >= s_begin && (st || out[0][0] == 12345.0)) {
       double d[kNR][4];
@@ -452,12 +532,6 @@ __global__ __launch_bounds__(256) void k_gauss_dog(const Pyramid P, const GaussL
     for (int i = 0; i < kNR; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
-    // The next scale's vertical pass, after this scale's stores: its
-    // registers do not overlap the epilogue's.
-    if (!L.db) __syncthreads();
-    if (s + 1 < s_end)
-      vert_any<OCT0, RMAX>(T, oc.rad[s + 1], (const cdouble*)(P.wts + oc.wofs[s + 1]), nxt);
-    __syncthreads();
   }
 }
 
@@ -486,15 +560,19 @@ bool gauss_needs_base0(const Pyramid& P) { return P.oct[0].rmax > kUR; }
 
 static bool staged0(const Pyramid& P, int o) { return o == 0 && !gauss_needs_base0(P); }
 
-// Strip row stride: covers the widest read of the horizontal pass (generic
-// path: 4 (kCG - 1) + round_up(2r + 4, 8)).
 constexpr int kSW0 = 2 * (kCG - 1) + 8 + 6;   // octave-0 strip stride for rmax <= 8
 constexpr int kSW1 = 2 * (kCG - 1) + kUR + 6;  // ... rmax <= kUR
 
+// Strip row stride (doubles).  Octaves >= 1: covers the widest read of the
+// horizontal pass (generic path: 4 (kCG - 1) + round_up(2r + 4, 8)), and is
+// 2 mod 4 so that the two rows a ds_read_b128 phase reads fall in disjoint
+// bank halves.
 static int strip_stride(const Pyramid& P, int o) {
   const int R = P.oct[o].rmax;
   if (staged0(P, o)) return R <= 8 ? kSW0 : kSW1;
-  return kGX + 2 * R + 12;
+  int sw = R <= kUR1 ? kGX + 2 * R + 4 : kGX + 2 * R + 12;
+  if (sw % 4 == 0) sw += 2;
+  return sw;
 }
 
 static size_t staged_bytes(const Pyramid& P, int o) {
@@ -503,12 +581,8 @@ static size_t staged_bytes(const Pyramid& P, int o) {
   return sizeof(double) * (size_t)(fl2(kGY - 1 + R) + cl2(R) + 1) * kBW0;
 }
 
-static bool double_buffer(const Pyramid& P, int o) {
-  return sizeof(double) * 2 * kGY * strip_stride(P, o) + staged_bytes(P, o) <= 64 * 1024;
-}
-
 size_t gauss_lds_bytes(const Pyramid& P, int o) {
-  return sizeof(double) * (double_buffer(P, o) ? 2 : 1) * kGY * strip_stride(P, o) + staged_bytes(P, o);
+  return sizeof(double) * kGY * strip_stride(P, o) + staged_bytes(P, o);
 }
 
 // Scale groups per octave: enough blocks to fill 256 CUs several times.
@@ -541,20 +615,19 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     set_attr<true, kSW0, 8>();
     set_attr<true, kSW1, kUR>();
-    set_attr<false, 0, kUR>();
+    set_attr<false, 0, kUR1>();
     attr_set = true;
   }
   L.sw = strip_stride(P, L.o);
-  L.db = double_buffer(P, L.o) ? 1 : 0;
   static const int dbg = [] { const char* e = std::getenv("SIFT_GAUSS_DBG"); return e ? std::atoi(e) : 0; }();
   L.dbg = dbg;
   const bool a16 = !((reinterpret_cast<uintptr_t>(L.dog)) & 15) &&
                    (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
   L.vec = (a16 && (oc.w & 3) == 0 && 4.0 * oc.h * oc.w < 2147483648.0) ? 1 : 0;
-  L.zero = oc.rmax > kUR ? 1 : 0;
+  L.zero = oc.rmax > (staged0(P, L.o) ? kUR : kUR1) ? 1 : 0;
   if (staged0(P, L.o) && L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8>), grid, dim3(256), lds, st, P, L);
   else if (staged0(P, L.o)) hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR>), grid, dim3(256), lds, st, P, L);
-  else hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR>), grid, dim3(256), lds, st, P, L);
+  else hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1>), grid, dim3(256), lds, st, P, L);
   return hipGetLastError();
 }
 

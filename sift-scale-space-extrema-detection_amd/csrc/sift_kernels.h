@@ -21,7 +21,6 @@ struct GaussLaunch {
   const double* base; // fp64 octave base h x w (o >= 1: the seed; o == 0: only when materialised)
   // filled by launch_gauss_dog
   int sw;             // strip row stride (doubles)
-  int db;             // double-buffered strips
   int vec;            // float4 plane stores are aligned
   int zero;           // strips need zeroing (generic-radius path present)
   int dbg;            // timing experiments (SIFT_GAUSS_DBG): bit 0 = no plane stores

@@ -13,7 +13,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "libsift_hip.so")
+LIB_PATH = os.environ.get("SIFT_HIP_LIB") or os.path.join(PKG_DIR, "libsift_hip.so")  # override: A/B builds
 
 SIFT_OK = 0
 SIFT_E_ARG = -1
