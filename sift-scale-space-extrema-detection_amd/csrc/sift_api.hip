@@ -53,6 +53,8 @@ enum DogSource { kNone = 0, kNative = 1, kForeign = 2 };
 struct sift_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;      // extrema scans of finished octaves, overlapping later octaves' Gaussians
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_oct[kMaxOctaves]{};
   std::string err;
   sift_params p{};
   int W = 0, H = 0;
@@ -69,6 +71,10 @@ struct sift_ctx {
   int slot_cap = 0;         // slots the refinement runs over
   bool ext_pending = false; // extrema launched, counts not yet read back
   bool has_keep = false;    // slots carry keep flags
+  bool scans_done = false;  // build_common already launched the extrema scans (side stream)
+  ExtremaLaunch xl{};       // extrema launch state between prepare / scan / finish
+  std::vector<long long> x_word_off, x_row_off;
+  long long x_rows = 0;
   // device memory
   DBuf img, seeds, gauss, dog, wts;
   DBuf base0;                                  // materialised octave-0 base (large radii only)
@@ -171,6 +177,19 @@ int sift_ctx_create(int device, sift_ctx** out) {
     return SIFT_E_HIP;
   }
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  // Measured on MI355X at 4K: overlapping the memory-bound scans with the
+  // small octaves' Gaussians slows both (shared L2/fabric), so the overlap
+  // is opt-in (SIFT_SIDE_STREAM=1).
+  if (std::getenv("SIFT_SIDE_STREAM") && std::atoi(std::getenv("SIFT_SIDE_STREAM"))) {
+    bool ok = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) == hipSuccess;
+    for (auto& e : ctx->ev_oct) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      (void)sift_ctx_destroy(ctx);
+      return SIFT_E_HIP;
+    }
+  }
   *out = ctx;
   return SIFT_OK;
 }
@@ -179,6 +198,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   if (!ctx) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
@@ -187,6 +207,11 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
+  for (auto& e : ctx->ev_oct)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SIFT_OK;
@@ -298,8 +323,14 @@ static long long total_plane_px(const sift_ctx* ctx) {
   return t;
 }
 
+static int extrema_prepare(sift_ctx* ctx, hipStream_t st);
+static int extrema_scan(sift_ctx* ctx, int o0, int o1, hipStream_t st);
+
+// overlap_extrema: launch each octave's extrema scan on the side stream as
+// soon as its DoG planes exist, overlapping the next octaves' Gaussian
+// kernels (memory-bound scans beside FMA-bound small octaves).
 static int build_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
-                        size_t stride, const sift_params* p, const double* sig) {
+                        size_t stride, const sift_params* p, const double* sig, bool overlap_extrema = false) {
   if (!ctx) return SIFT_E_ARG;
   if (!img_host && !img_dev) return set_err(ctx, SIFT_E_ARG, "null image");
   if (stride < (size_t)W) return set_err(ctx, SIFT_E_ARG, "stride < width");
@@ -333,6 +364,15 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     HIPCHK(launch_upsample_base(P, ctx->base0.as<double>(), ctx->stream));
     base0 = ctx->base0.as<double>();
   }
+  ctx->scans_done = false;
+  const bool overlap = overlap_extrema && ctx->side;
+  if (overlap) {  // the side stream starts after this image's setup, resets the extrema counters
+    ctx->dog_source = kNative;
+    HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    rc = extrema_prepare(ctx, ctx->side);
+    if (rc) return rc;
+  }
   for (int o = 0; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
     GaussLaunch L{};
@@ -343,8 +383,20 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off : nullptr;
     L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : 0;
     HIPCHK(launch_gauss_dog(P, L, ctx->stream));
+    if (overlap) {
+      HIPCHK(hipEventRecord(ctx->ev_oct[o], ctx->stream));
+      HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_oct[o], 0));
+      rc = extrema_scan(ctx, o, o + 1, ctx->side);
+      if (rc) return rc;
+    }
   }
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+  if (overlap) {
+    HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));  // extrema_ms: what the overlap did not hide
+    HIPCHK(hipEventRecord(ctx->ev_join, ctx->side));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    ctx->scans_done = true;
+  }
   ctx->dog_source = kNative;
   ctx->have_gauss = keep_gauss;
   ctx->have_cand = false;
@@ -488,22 +540,29 @@ static float round_toward(double v, int dir) {
 enum { kCntAmb = 0, kCntLow = 1, kCntDrop = 2, kCntUnc = 3, kCntSing = 4, kCntN = 12, kCntKp = 13 };
 constexpr int kRetry = 1;  // internal: a capacity overflowed, grow and run again
 
-// Launches the extrema stage without waiting: bitmap scan, ordered emission
-// into cand_cap slots, exact tie resolution.  Counts stay on the device.
-static int launch_extrema_stage(sift_ctx* ctx) {
+// The extrema stage, launched without waiting, in three parts:
+//   extrema_prepare  capacities, buffers, counter resets (on stream st);
+//   extrema_scan     bitmap scan of octaves [o0, o1) (k_extrema) on st --
+//                    detect overlaps it with the later octaves' Gaussians;
+//   extrema_finish   row-count scan, ordered emission into cand_cap slots,
+//                    exact tie resolution (context stream).
+// Counts stay on the device.
+static int extrema_prepare(sift_ctx* ctx, hipStream_t st) {
   Pyramid& P = ctx->P;
   const bool exact_planes = ctx->dog_source == kForeign;
   unsigned* cnt = ctx->counters.as<unsigned>();
   // Row / word geometry of the candidate bitmap.
-  std::vector<long long> word_off(P.O), row_off(P.O);
+  ctx->x_word_off.assign(P.O, 0);
+  ctx->x_row_off.assign(P.O, 0);
   long long words = 0, rows = 0;
   for (int o = 0; o < P.O; ++o) {
     const int nw = extrema_words_per_row(P.oct[o].w);
-    word_off[o] = words;
-    row_off[o] = rows;
+    ctx->x_word_off[o] = words;
+    ctx->x_row_off[o] = rows;
     words += (long long)P.S * P.oct[o].h * nw;
     rows += (long long)P.S * P.oct[o].h;
   }
+  ctx->x_rows = rows;
   {  // capacities: an estimate for this geometry, grown on overflow (settle_extrema)
     const long long est = std::min<long long>(std::max<long long>((long long)P.S * total_plane_px(ctx) / 192, 65536),
                                               0x7fffffffLL);
@@ -520,23 +579,34 @@ static int launch_extrema_stage(sift_ctx* ctx) {
   // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
   // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
   const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
-  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), ctx->stream));
-  HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), ctx->stream));
-  ExtremaLaunch L{};
+  HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), st));
+  HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), st));
+  ExtremaLaunch& L = ctx->xl;
+  L = ExtremaLaunch{};
   L.exact_planes = exact_planes;
   L.c_lo = exact_planes ? t_up : t_dn;
   L.c_hi = exact_planes ? t_up : std::nextafter(t_up, INFINITY);
   L.bitmap = ctx->bitmap.as<unsigned long long>();
   L.rowcount = ctx->rowcount.as<unsigned>();
   for (int o = 0; o < P.O; ++o) {
-    L.word_off[o] = word_off[o];
-    L.row_off[o] = (int)row_off[o];
+    L.word_off[o] = ctx->x_word_off[o];
+    L.row_off[o] = (int)ctx->x_row_off[o];
   }
   L.amb_keys = ctx->amb_keys.as<unsigned>();
   L.counters = cnt;
   L.amb_cap = ctx->amb_cap;
-  HIPCHK(launch_extrema(P, L, ctx->stream));
+  return SIFT_OK;
+}
+
+static int extrema_scan(sift_ctx* ctx, int o0, int o1, hipStream_t st) {
+  HIPCHK(launch_extrema(ctx->P, ctx->xl, st, o0, o1));
+  return SIFT_OK;
+}
+
+static int extrema_finish(sift_ctx* ctx) {
+  Pyramid& P = ctx->P;
+  unsigned* cnt = ctx->counters.as<unsigned>();
+  const long long rows = ctx->x_rows;
   size_t tb = 0;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
                                           (int)(rows + 1), ctx->stream));
@@ -549,11 +619,11 @@ static int launch_extrema_stage(sift_ctx* ctx) {
   for (int o = 0; o < P.O; ++o) {
     EmitLaunch E{};
     E.o = o;
-    E.bitmap = ctx->bitmap.as<unsigned long long>() + word_off[o];
+    E.bitmap = ctx->bitmap.as<unsigned long long>() + ctx->x_word_off[o];
     E.nw = extrema_words_per_row(P.oct[o].w);
-    E.rowcount = ctx->rowcount.as<unsigned>() + row_off[o];
+    E.rowcount = ctx->rowcount.as<unsigned>() + ctx->x_row_off[o];
     E.rowoff = ctx->rowoff.as<unsigned>();
-    E.row_base = (int)row_off[o];
+    E.row_base = (int)ctx->x_row_off[o];
     E.keys = ctx->cand_key.as<unsigned>();
     E.value = ctx->cand_val.as<double>();
     E.keep = ctx->cand_keep.as<unsigned>();
@@ -575,6 +645,16 @@ static int launch_extrema_stage(sift_ctx* ctx) {
   ctx->has_keep = true;
   ctx->ext_pending = true;
   return SIFT_OK;
+}
+
+// The whole extrema stage on the context stream.
+static int launch_extrema_stage(sift_ctx* ctx) {
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  int rc = extrema_prepare(ctx, ctx->stream);
+  if (rc) return rc;
+  rc = extrema_scan(ctx, 0, ctx->P.O, ctx->stream);
+  if (rc) return rc;
+  return extrema_finish(ctx);
 }
 
 // Reads the extrema counts (ctx->h_counters must hold the device counters):
@@ -810,12 +890,17 @@ static int detect_common(sift_ctx* ctx, const float* img_host, const float* img_
                          size_t stride, const sift_params* p, sift_keypoint* out, size_t cap,
                          size_t* n_out) {
   if (!ctx) return SIFT_E_ARG;
-  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr);
+  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, true);
   if (rc) return rc;
   // One host synchronisation per image; a capacity overflow (first images)
   // grows the buffers and reruns extrema + refinement.
   do {
-    rc = launch_extrema_stage(ctx);
+    if (ctx->scans_done) {
+      ctx->scans_done = false;
+      rc = extrema_finish(ctx);
+    } else {
+      rc = launch_extrema_stage(ctx);
+    }
     if (rc) return rc;
     rc = run_refine(ctx);
   } while (rc == kRetry);

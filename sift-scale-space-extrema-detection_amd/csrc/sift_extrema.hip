@@ -217,8 +217,8 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
 // is reduced once (3-wide max/min with DPP shifts) and shared by the scales
 // above and below it; the decisions are SALU lane-mask logic.
 __global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
-  const int u = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (u >= L.unit_off[L.n_oct]) return;
+  const int u = L.u_begin + (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (u >= L.u_end) return;
   int o = 0;
   while (o + 1 < L.n_oct && u >= L.unit_off[o + 1]) ++o;
   int loc = u - L.unit_off[o];
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
   }
 }
 
-hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st) {
+hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, int o_begin, int o_end) {
   L.n_oct = P.O;
   L.ng = (P.S + kXMaxGroup - 1) / kXMaxGroup;
   int units = 0;
@@ -335,11 +335,13 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st) {
     if (oc.h >= 3 && oc.w >= 3 && P.S >= 1) units += L.ng * L.nw[o] * ((oc.h - 2 + kXRows - 1) / kXRows);
   }
   L.unit_off[P.O] = units;
-  if (units == 0) return hipSuccess;
+  L.u_begin = L.unit_off[o_begin];
+  L.u_end = L.unit_off[o_end];
+  if (L.u_end <= L.u_begin) return hipSuccess;
   // 32-bit buffer offsets cover one scale group's planes
   const int np = std::min(P.S, kXMaxGroup) + 2;
   if (4.0 * np * (double)P.oct[0].h * P.oct[0].w >= 4294967296.0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_extrema, dim3((units + 3) / 4), dim3(256), 0, st, P, L);
+  hipLaunchKernelGGL(k_extrema, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), 0, st, P, L);
   return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ constexpr int kXMaxGroup = 5;// scales per extrema wave (S > 5 splits the scales
 // rows, 62-column word, scale group).
 struct ExtremaLaunch {
   int n_oct;
+  int u_begin, u_end;            // units of this launch (a range of octaves)
   int exact_planes;              // DoG planes are the data itself (caller-supplied): no fp32 ties
   int ng;                        // scale groups per (strip, word)
   float c_lo, c_hi;              // |v| < c_lo: certainly low contrast; |v| >= c_hi: certainly not
@@ -96,7 +97,7 @@ hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int 
 
 // Fills the unit table of L (octave geometry) and launches the scan; returns
 // the launch error.  L.bitmap words per octave: S * h * nw.
-hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st);
+hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, int o_begin, int o_end);
 inline int extrema_words_per_row(int w) { return (w + kXW - 1) / kXW; }
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st);
 // One wave per ambiguous candidate: fp64 pointwise recompute of the 3x3x3 DoG patch.
