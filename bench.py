@@ -11,11 +11,15 @@ keypoint lists are all-gathered over RCCL (xGMI) each step: weak scaling.
 Prints ONE JSON line (rank 0).  Workload defaults to BASELINE.json's metric
 configuration: 3840x2160 (4K), 4 octaves x 5 scales.
 
-Roofline of the dominant kernel (k_gauss_dog, HBM-bound): algorithmic bytes
-B_alg = 4WH + sum_o 4 P_o (S+3) + sum_o 4 P_o (S+2) (input
-read + Gaussian and DoG planes written, fp32), divided by the kernel's
-HIP-event time on the context's stream.  `traffic` comes from the committed
-rocprofv3 PMC summary (profiles/*pmc*.json) when it matches the config.
+Roofline of the dominant kernel -- octave 0's k_gauss_dog launch, HBM-bound
+on its plane stores: algorithmic bytes per launch 4WH + 4 P_0 (S+3) +
+4 P_0 (S+2) (the input read, octave 0's Gaussian and DoG planes written in
+fp32; SURVEY.md §8d per octave), divided by that launch's HIP-event time on
+the context's stream (sift_timings.gauss_oct0_ms).  `traffic` is that
+kernel's HBM bytes per launch from the committed rocprofv3 PMC summary
+(profiles/*pmc*.json, tools/pmc_traffic.py) when it matches the config.
+`stage` reports the whole Gaussian+DoG pass (all octaves, one launch each)
+the same way: B_alg = 4WH + sum_o 4 P_o (S+3) + sum_o 4 P_o (S+2).
 """
 import argparse
 import glob
@@ -50,8 +54,14 @@ def alg_bytes(W, H, O, S, skip_gauss):
     return b
 
 
+def oct0_bytes(W, H, S, skip_gauss):
+    """Algorithmic bytes of octave 0's Gaussian+DoG launch."""
+    h, w = octave_dims(W, H, 1)[0]
+    return 4 * W * H + 4 * h * w * (S + 2) + (0 if skip_gauss else 4 * h * w * (S + 3))
+
+
 def load_traffic(cfg_key):
-    """Per-launch HBM bytes of k_gauss_dog from a committed PMC summary."""
+    """Per-launch HBM bytes of octave 0's k_gauss_dog from a committed PMC summary."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
@@ -142,7 +152,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     ctx.synchronize()
-    stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0}
+    stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0, "gauss_oct0_ms": 0.0}
     t0 = time.perf_counter()
     n_total = 0
     for _ in range(args.steps):
@@ -166,9 +176,11 @@ def main():
 
     if rank == 0:
         gauss_ms = stage["gauss_dog_ms"] / K
+        oct0_ms = stage["gauss_oct0_ms"] / K
         B = alg_bytes(W, H, O, S, args.skip_gauss_planes)
-        launches = O  # one k_gauss_dog launch per octave
-        achieved = (B / launches) / (gauss_ms / launches * 1e-3) / 1e9
+        B0 = oct0_bytes(W, H, S, args.skip_gauss_planes)
+        achieved = B0 / (oct0_ms * 1e-3) / 1e9
+        stage_achieved = B / (gauss_ms * 1e-3) / 1e9
         cfg_key = "%dx%d_o%d_s%d%s" % (W, H, O, S, "_nogauss" if args.skip_gauss_planes else "")
         traffic, traffic_src = load_traffic(cfg_key)
         out = {
@@ -199,17 +211,26 @@ def main():
             "keypoints_all_ranks": n_total,
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_gauss_dog",
+                "kernel": "k_gauss_dog (octave 0)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "alg_bytes_per_launch": B / launches,
-                "alg_bytes_formula": ("4WH + sum_o 4P_o(S+2) + sum_{o>=1} 8P_o" if args.skip_gauss_planes
-                                      else "4WH + sum_o 4P_o(S+3) + sum_o 4P_o(S+2)"),
-                "launch_ms": round(gauss_ms / launches, 5),
+                "alg_bytes_per_launch": B0,
+                "alg_bytes_formula": ("4WH + 4P_0(S+2)" if args.skip_gauss_planes
+                                      else "4WH + 4P_0(S+3) + 4P_0(S+2)"),
+                "launch_ms": round(oct0_ms, 5),
+                "stage": {
+                    "what": "whole Gaussian+DoG pass, %d launches (one per octave)" % O,
+                    "alg_bytes": B,
+                    "alg_bytes_formula": ("4WH + sum_o 4P_o(S+2) + sum_{o>=1} 8P_o" if args.skip_gauss_planes
+                                          else "4WH + sum_o 4P_o(S+3) + sum_o 4P_o(S+2)"),
+                    "ms": round(gauss_ms, 5),
+                    "achieved": round(stage_achieved, 1),
+                    "frac": round(stage_achieved / HBM_PEAK_GBS, 4),
+                },
             },
             "cpu_baseline": None,
         }

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 1
+#define SIFT_ABI_VERSION 2
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -97,6 +97,8 @@ typedef struct {
   double extrema_ms;   /* extrema scan + ordering + exact tie resolution    */
   double refine_ms;    /* refinement + compaction                           */
   double h2d_ms;       /* input upload (0 for the device-pointer entry)     */
+  double gauss_oct0_ms;/* octave 0's Gaussian + DoG launch alone (the        */
+                       /* dominant, HBM-bound kernel; ABI version >= 2)     */
 } sift_timings;
 
 int sift_abi_version(void);

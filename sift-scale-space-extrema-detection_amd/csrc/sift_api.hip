@@ -383,6 +383,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off : nullptr;
     L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : 0;
     HIPCHK(launch_gauss_dog(P, L, ctx->stream));
+    if (o == 0) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     if (overlap) {
       HIPCHK(hipEventRecord(ctx->ev_oct[o], ctx->stream));
       HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_oct[o], 0));
@@ -415,6 +416,7 @@ int sift_build_scale_space(sift_ctx* ctx, const float* img, int width, int heigh
   (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
   ctx->tm.h2d_ms = a;
   ctx->tm.gauss_dog_ms = b;
+  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
   return SIFT_OK;
 }
 
@@ -427,6 +429,7 @@ int sift_build_scale_space_device(sift_ctx* ctx, const float* d_img, int width, 
   (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
   ctx->tm.h2d_ms = 0;
   ctx->tm.gauss_dog_ms = b;
+  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
   return SIFT_OK;
 }
 
@@ -910,6 +913,7 @@ static int detect_common(sift_ctx* ctx, const float* img_host, const float* img_
   if (img_host && hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->tm.h2d_ms = a;
   if (!img_host) ctx->tm.h2d_ms = 0;
   if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]) == hipSuccess) ctx->tm.gauss_dog_ms = b;
+  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
   read_stage_times(ctx, true, true);
   rc = sift_copy_keypoints(ctx, out, cap, n_out);
   if (rc) return rc;

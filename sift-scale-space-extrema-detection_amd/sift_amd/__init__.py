@@ -74,7 +74,8 @@ class Keypoint(ctypes.Structure):
 
 class Timings(ctypes.Structure):
     _fields_ = [("gauss_dog_ms", ctypes.c_double), ("extrema_ms", ctypes.c_double),
-                ("refine_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double)]
+                ("refine_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+                ("gauss_oct0_ms", ctypes.c_double)]
 
 
 EXTREMUM_DTYPE = np.dtype([("octave", "<i4"), ("scale", "<i4"), ("x", "<i4"), ("y", "<i4"),
@@ -340,7 +341,7 @@ class Context:
         t = Timings()
         self._check(self._L.sift_last_timings(self._h, ctypes.byref(t)), "sift_last_timings")
         return dict(gauss_dog_ms=t.gauss_dog_ms, extrema_ms=t.extrema_ms, refine_ms=t.refine_ms,
-                    h2d_ms=t.h2d_ms)
+                    h2d_ms=t.h2d_ms, gauss_oct0_ms=t.gauss_oct0_ms)
 
     def stream(self):
         return self._L.sift_stream(self._h)

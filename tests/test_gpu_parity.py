@@ -192,3 +192,26 @@ def test_skip_gauss_planes_same_keypoints(gpu_ctx):
     assert a.tobytes() == b.tobytes()
     with pytest.raises(sift_amd.SiftError):
         gpu_ctx.plane(sift_amd.PLANE_GAUSS, 0, 0)
+
+
+def test_large_radii_paths_match_oracle(gpu_ctx):
+    """min_blur 2.5: octave-0 radii above the unrolled range (materialised
+    fp64 upsample + generic-radius path) and radii up to ~45 in octave 1."""
+    img = blob_image(160, 120, seed=31)
+    p = sift_amd.make_params(3, 3, min_blur=2.5)
+    kp = gpu_ctx.detect(img, p)
+    r = orc.OracleRun(img, _oracle_params(p), orc.CONV_SEPARABLE)
+    check_candidates(gpu_ctx.candidates(), r.candidates())
+    check_keypoints(kp, r.refined)
+    assert gpu_ctx.counts()["low_contrast"] == r.n_low
+
+
+@pytest.mark.parametrize("W,H", [(257, 131), (64, 48)])
+def test_unaligned_widths_match_oracle(gpu_ctx, W, H):
+    """Widths not a multiple of 4 (scalar plane stores, ragged right tiles)."""
+    img = blob_image(W, H, seed=W + H)
+    p = sift_amd.make_params(4, 4)
+    kp = gpu_ctx.detect(img, p)
+    r = orc.OracleRun(img, _oracle_params(p), orc.CONV_SEPARABLE)
+    check_candidates(gpu_ctx.candidates(), r.candidates())
+    check_keypoints(kp, r.refined)
