@@ -99,6 +99,12 @@ def main():
     ap.add_argument("--scales", type=int, default=5)
     ap.add_argument("--skip-gauss-planes", action="store_true",
                     help="keypoints-only mode: do not materialise the Gaussian planes")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="detections in flight per GPU: contexts on ONE stream, so image k+1 is queued "
+                         "behind image k (no kernel overlap) while the host settles image k")
+    ap.add_argument("--independent-streams", action="store_true",
+                    help="in-flight detections on their own streams: kernels of consecutive images overlap "
+                         "(higher Mpix/s; per-kernel durations, hence roofline.achieved, include the overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
     args = ap.parse_args()
@@ -129,38 +135,51 @@ def main():
     img = blob_image(W, H, seed=42 + rank)
     d_img = torch.from_numpy(img).to("cuda:%d" % dev)
     torch.cuda.synchronize(dev)
-    ctx = sift_amd.Context(dev)
+    nin = max(1, args.inflight)
+    ctxs = [sift_amd.Context(dev)]
+    ctxs += [sift_amd.Context(dev, share=None if args.independent_streams else ctxs[0]) for _ in range(nin - 1)]
+    ctx = ctxs[0]
 
     gather = None
     if dist is not None:
         from sift_amd.dist import KeypointGather
         gather = KeypointGather("cuda:%d" % dev)
 
-    def all_gather_keypoints(n):
-        counts = gather(n, lambda buf, cap: ctx.copy_keypoints_device(buf.data_ptr(), cap))
-        return sum(counts)
+    stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0, "gauss_oct0_ms": 0.0}
 
-    def step():
-        n = ctx.detect_device(d_img.data_ptr(), W, H, params)
+    def launch(i):
+        ctxs[i % nin].detect_device_async(d_img.data_ptr(), W, H, params)
+
+    def finish(i, acc):
+        c = ctxs[i % nin]
+        n = c.detect_wait()
         if dist is not None:
-            n = all_gather_keypoints(n)
+            n = sum(gather(n, lambda buf, cap: c.copy_keypoints_device(buf.data_ptr(), cap)))
+        if acc:
+            t = c.timings()
+            for k in stage:
+                stage[k] += t[k]
         return n
 
-    for _ in range(args.warmup):
-        step()
+    # Warm-up: every context settles its capacities synchronously first.
+    for i in range(max(args.warmup, nin)):
+        launch(i)
+        finish(i, False)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ctx.synchronize()
-    stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0, "gauss_oct0_ms": 0.0}
+    for c in ctxs:
+        c.synchronize()
     t0 = time.perf_counter()
     n_total = 0
-    for _ in range(args.steps):
-        n_total = step()
-        t = ctx.timings()
-        for k in stage:
-            stage[k] += t[k]
-    ctx.synchronize()
+    for i in range(args.steps):  # image i is enqueued before image i-(nin-1) is settled
+        launch(i)
+        if i >= nin - 1:
+            n_total = finish(i - (nin - 1), True)
+    for i in range(max(0, args.steps - (nin - 1)), args.steps):
+        n_total = finish(i, True)
+    for c in ctxs:
+        c.synchronize()
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -172,7 +191,7 @@ def main():
     K = args.steps
     ms_per_step = elapsed / K * 1e3
     value = world * W * H / (elapsed / K) / 1e6
-    counts = ctx.counts()
+    counts = ctxs[(args.steps - 1) % nin].counts()
 
     if rank == 0:
         gauss_ms = stage["gauss_dog_ms"] / K
@@ -201,7 +220,8 @@ def main():
                             "Gaussian+DoG+extrema+refine (keypoints out)%s" %
                             (W, H, O, S, ", Gaussian planes not materialised" if args.skip_gauss_planes else ""),
                 "width": W, "height": H, "octaves": O, "scales_per_octave": S,
-                "images_per_gpu": 1, "global_batch": world,
+                "images_per_gpu": 1, "global_batch": world, "inflight_per_gpu": nin,
+                "streams_per_gpu": nin if args.independent_streams else 1,
                 "parallelism": "dp%d (one image per GPU, RCCL keypoint all-gather)" % world if world > 1 else "single GPU",
                 "planes": "fp32 out, fp64 accumulation/seeds",
             },
@@ -238,7 +258,8 @@ def main():
             sw, sh = (int(v) for v in args.cpu_sample.split("x"))
             out["cpu_baseline"] = cpu_baseline(img, O, S, min(sw, W), min(sh, H))
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in reversed(ctxs):
+        c.close()
     if dist is not None:
         dist.destroy_process_group()
     return 0

@@ -106,6 +106,11 @@ int sift_params_default(sift_params *p);
 
 /* Context: owns one HIP stream and device-resident pyramids on `device`. */
 int sift_ctx_create(int device, struct sift_ctx **out);
+/* A context on the SAME stream as `share` (ABI version >= 2): its work is
+ * ordered after everything already enqueued on `share`, so several
+ * detections can be in flight (sift_detect_device_async) without their
+ * kernels overlapping.  Destroy it before `share`. */
+int sift_ctx_create_shared(struct sift_ctx *share, struct sift_ctx **out);
 int sift_ctx_destroy(struct sift_ctx *ctx);
 const char *sift_last_error(struct sift_ctx *ctx);
 
@@ -190,6 +195,15 @@ int sift_detect_device(struct sift_ctx *ctx, const float *d_img, int width, int 
  * extrema, refined keypoints, singular Hessians, exact fp64 re-decisions. */
 int sift_last_counts(struct sift_ctx *ctx, size_t *n_candidates, size_t *n_low_contrast,
                      size_t *n_keypoints, size_t *n_singular, size_t *n_exact);
+
+/* Asynchronous one-call detection (ABI version >= 2): enqueue on the
+ * context's stream and return; sift_detect_wait completes it (one host
+ * synchronisation, capacity retries, counts) and copies the keypoints like
+ * sift_detect.  One detection in flight per context: several contexts
+ * (streams) keep the device busy while the host settles earlier images. */
+int sift_detect_device_async(struct sift_ctx *ctx, const float *d_img, int width, int height,
+                             size_t stride_px, const sift_params *p);
+int sift_detect_wait(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out);
 
 int sift_last_timings(struct sift_ctx *ctx, sift_timings *t);
 

@@ -53,6 +53,7 @@ enum DogSource { kNone = 0, kNative = 1, kForeign = 2 };
 struct sift_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  bool own_stream = true;          // false: the stream of another context (sift_ctx_create_shared)
   hipStream_t side = nullptr;      // extrema scans of finished octaves, overlapping later octaves' Gaussians
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_oct[kMaxOctaves]{};
   std::string err;
@@ -72,12 +73,16 @@ struct sift_ctx {
   bool ext_pending = false; // extrema launched, counts not yet read back
   bool has_keep = false;    // slots carry keep flags
   bool scans_done = false;  // build_common already launched the extrema scans (side stream)
+  bool counters_zeroed = false;  // extrema_prepare zeroed the refinement counters too
+  bool detect_pending = false;   // sift_detect_device_async enqueued, sift_detect_wait not yet called
+  bool detect_host_img = false;
   ExtremaLaunch xl{};       // extrema launch state between prepare / scan / finish
   std::vector<long long> x_word_off, x_row_off;
   long long x_rows = 0;
   // device memory
   DBuf img, seeds, gauss, dog, wts;
   DBuf base0;                                  // materialised octave-0 base (large radii only)
+  std::vector<double> wts_host;                // taps last uploaded to wts
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
   DBuf keep, pos;                              // keypoint compaction
@@ -161,7 +166,7 @@ int sift_schedule(const sift_params* p, double* blur, double* sigma) {
   return SIFT_OK;
 }
 
-int sift_ctx_create(int device, sift_ctx** out) {
+static int ctx_create(int device, sift_ctx* share, sift_ctx** out) {
   if (!out) return SIFT_E_ARG;
   *out = nullptr;
   int n = 0;
@@ -169,8 +174,10 @@ int sift_ctx_create(int device, sift_ctx** out) {
   if (device < 0 || device >= n) return SIFT_E_ARG;
   sift_ctx* ctx = new sift_ctx();
   ctx->device = device;
+  ctx->own_stream = share == nullptr;
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      (share ? (ctx->stream = share->stream, false)
+             : hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) ||
       hipHostMalloc((void**)&ctx->h_counters, 64 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
       ctx->counters.ensure(64 * sizeof(unsigned)) != hipSuccess) {
     delete ctx;
@@ -194,6 +201,13 @@ int sift_ctx_create(int device, sift_ctx** out) {
   return SIFT_OK;
 }
 
+int sift_ctx_create(int device, sift_ctx** out) { return ctx_create(device, nullptr, out); }
+
+int sift_ctx_create_shared(sift_ctx* share, sift_ctx** out) {
+  if (!share || !out) return SIFT_E_ARG;
+  return ctx_create(share->device, share, out);
+}
+
 int sift_ctx_destroy(sift_ctx* ctx) {
   if (!ctx) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
@@ -212,7 +226,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SIFT_OK;
 }
@@ -306,11 +320,14 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
     if (gauss_lds_bytes(P, o) > 160 * 1024)
       return set_err(ctx, SIFT_E_UNSUPPORTED, "blur radius too large for one LDS strip");
   if (need_weights) {
-    if (ctx->wts.ensure(w.size() * sizeof(double)) != hipSuccess)
-      return set_err(ctx, SIFT_E_HIP, "hipMalloc weights");
-    if (hipMemcpyAsync(ctx->wts.p, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice,
-                       ctx->stream) != hipSuccess)
-      return set_err(ctx, SIFT_E_HIP, "upload weights");
+    // Upload only when the taps changed (the same schedule image after image).
+    if (w != ctx->wts_host || !ctx->wts.p) {
+      if (ctx->wts.ensure(w.size() * sizeof(double)) != hipSuccess)
+        return set_err(ctx, SIFT_E_HIP, "hipMalloc weights");
+      if (hipMemcpy(ctx->wts.p, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+        return set_err(ctx, SIFT_E_HIP, "upload weights");
+      ctx->wts_host = w;
+    }
     P.wts = ctx->wts.as<double>();
   }
   (void)soff;
@@ -582,7 +599,8 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st) {
   // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
   // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
   const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
-  HIPCHK(hipMemsetAsync(cnt, 0, 16 * sizeof(unsigned), st));
+  HIPCHK(hipMemsetAsync(cnt, 0, 32 * sizeof(unsigned), st));  // extrema and refinement counters
+  ctx->counters_zeroed = true;
   HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), st));
   ExtremaLaunch& L = ctx->xl;
   L = ExtremaLaunch{};
@@ -619,14 +637,18 @@ static int extrema_finish(sift_ctx* ctx) {
                                           (int)(rows + 1), ctx->stream));
   HIPCHK(hipMemcpyAsync(cnt + kCntN, ctx->rowoff.as<unsigned>() + rows, sizeof(unsigned), hipMemcpyDeviceToDevice,
                         ctx->stream));
-  for (int o = 0; o < P.O; ++o) {
+  {
     EmitLaunch E{};
-    E.o = o;
-    E.bitmap = ctx->bitmap.as<unsigned long long>() + ctx->x_word_off[o];
-    E.nw = extrema_words_per_row(P.oct[o].w);
-    E.rowcount = ctx->rowcount.as<unsigned>() + ctx->x_row_off[o];
+    E.n_oct = P.O;
+    for (int o = 0; o < P.O; ++o) {
+      E.row_off[o] = (int)ctx->x_row_off[o];
+      E.word_off[o] = ctx->x_word_off[o];
+      E.nw[o] = extrema_words_per_row(P.oct[o].w);
+    }
+    E.row_off[P.O] = (int)rows;
+    E.bitmap = ctx->bitmap.as<unsigned long long>();
+    E.rowcount = ctx->rowcount.as<unsigned>();
     E.rowoff = ctx->rowoff.as<unsigned>();
-    E.row_base = (int)ctx->x_row_off[o];
     E.keys = ctx->cand_key.as<unsigned>();
     E.value = ctx->cand_val.as<double>();
     E.keep = ctx->cand_keep.as<unsigned>();
@@ -692,9 +714,9 @@ static int run_extrema(sift_ctx* ctx) {
 }
 
 // Refinement over ctx->slot_cap slots, *counters[12] of them live, without
-// a host round trip; one synchronisation at the end reads every count back.
-// Returns kRetry when the extrema stage it follows overflowed.
-static int run_refine(sift_ctx* ctx) {
+// a host round trip; refine_settle's one synchronisation reads every count
+// back and returns kRetry when the extrema stage it follows overflowed.
+static int refine_enqueue(sift_ctx* ctx) {
   Pyramid& P = ctx->P;
   const int cap = ctx->slot_cap;
   unsigned* cnt = ctx->counters.as<unsigned>();
@@ -705,9 +727,12 @@ static int run_refine(sift_ctx* ctx) {
   HIPCHK(ctx->uncertain.ensure((size_t)std::max(cap, 1) * sizeof(unsigned)));
   HIPCHK(ctx->keep.ensure((size_t)std::max(cap, 1) * sizeof(unsigned)));
   HIPCHK(ctx->pos.ensure((size_t)std::max(cap, 1) * sizeof(unsigned)));
-  HIPCHK(hipMemsetAsync(cnt + kCntUnc, 0, 2 * sizeof(unsigned), ctx->stream));
-  HIPCHK(hipMemsetAsync(cnt + kCntKp, 0, sizeof(unsigned), ctx->stream));
-  HIPCHK(hipMemsetAsync(cnt + 16, 0, 16 * sizeof(unsigned), ctx->stream));
+  if (!ctx->counters_zeroed) {  // refinement without a fresh extrema stage (caller candidates / re-run)
+    HIPCHK(hipMemsetAsync(cnt + kCntUnc, 0, 2 * sizeof(unsigned), ctx->stream));
+    HIPCHK(hipMemsetAsync(cnt + kCntKp, 0, sizeof(unsigned), ctx->stream));
+    HIPCHK(hipMemsetAsync(cnt + 16, 0, 16 * sizeof(unsigned), ctx->stream));
+  }
+  ctx->counters_zeroed = false;
   ctx->n_kp = 0;
   ctx->n_sing = 0;
   if (cap > 0) {
@@ -741,7 +766,14 @@ static int run_refine(sift_ctx* ctx) {
   }
   HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 32 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+// Waits for the refinement enqueued by refine_enqueue and reads its counts
+// (and the extrema counts when those are still pending).
+static int refine_settle(sift_ctx* ctx) {
+  const int cap = ctx->slot_cap;
+  HIPCHK(hipEventSynchronize(ctx->ev[6]));
   if (ctx->ext_pending) {
     const int rc = settle_extrema(ctx);
     if (rc) return rc;
@@ -758,6 +790,11 @@ static int run_refine(sift_ctx* ctx) {
                  "refine uncertain %u: det %u alpha %u omega %u edge_dt %u edge_int %u round %u | iter %u %u %u %u %u\n",
                  h[kCntUnc], h[16], h[17], h[18], h[19], h[20], h[21], h[22], h[23], h[24], h[25], h[26]);
   return SIFT_OK;
+}
+
+static int run_refine(sift_ctx* ctx) {
+  const int rc = refine_enqueue(ctx);
+  return rc ? rc : refine_settle(ctx);
 }
 
 static void read_stage_times(sift_ctx* ctx, bool extrema, bool refine) {
@@ -889,29 +926,44 @@ int sift_refine(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out, si
   return SIFT_OK;
 }
 
-static int detect_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
-                         size_t stride, const sift_params* p, sift_keypoint* out, size_t cap,
-                         size_t* n_out) {
+// Enqueues one whole detection (Gaussian+DoG, extrema, refinement) without
+// waiting; detect_finish completes it.
+static int detect_enqueue(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
+                          size_t stride, const sift_params* p) {
   if (!ctx) return SIFT_E_ARG;
   int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, true);
   if (rc) return rc;
-  // One host synchronisation per image; a capacity overflow (first images)
-  // grows the buffers and reruns extrema + refinement.
-  do {
-    if (ctx->scans_done) {
-      ctx->scans_done = false;
-      rc = extrema_finish(ctx);
-    } else {
-      rc = launch_extrema_stage(ctx);
-    }
+  if (ctx->scans_done) {
+    ctx->scans_done = false;
+    rc = extrema_finish(ctx);
+  } else {
+    rc = launch_extrema_stage(ctx);
+  }
+  if (rc) return rc;
+  rc = refine_enqueue(ctx);
+  if (rc) return rc;
+  ctx->detect_pending = true;
+  ctx->detect_host_img = img_host != nullptr;
+  return SIFT_OK;
+}
+
+// One host synchronisation per image; a capacity overflow (first images)
+// grows the buffers and reruns extrema + refinement.
+static int detect_finish(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->detect_pending) return set_err(ctx, SIFT_E_STATE, "no detection in flight");
+  ctx->detect_pending = false;
+  int rc = refine_settle(ctx);
+  while (rc == kRetry) {
+    rc = launch_extrema_stage(ctx);
     if (rc) return rc;
     rc = run_refine(ctx);
-  } while (rc == kRetry);
+  }
   if (rc) return rc;
   float a = 0, b = 0;
   (void)hipEventSynchronize(ctx->ev[6]);
-  if (img_host && hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->tm.h2d_ms = a;
-  if (!img_host) ctx->tm.h2d_ms = 0;
+  if (ctx->detect_host_img && hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->tm.h2d_ms = a;
+  if (!ctx->detect_host_img) ctx->tm.h2d_ms = 0;
   if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]) == hipSuccess) ctx->tm.gauss_dog_ms = b;
   if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
   read_stage_times(ctx, true, true);
@@ -919,6 +971,27 @@ static int detect_common(sift_ctx* ctx, const float* img_host, const float* img_
   if (rc) return rc;
   if (ctx->n_sing) return set_err(ctx, SIFT_E_SINGULAR, "singular Hessian (the reference throws a TypeError here)");
   return SIFT_OK;
+}
+
+static int detect_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
+                         size_t stride, const sift_params* p, sift_keypoint* out, size_t cap,
+                         size_t* n_out) {
+  const int rc = detect_enqueue(ctx, img_host, img_dev, W, H, stride, p);
+  return rc ? rc : detect_finish(ctx, out, cap, n_out);
+}
+
+int sift_detect_device_async(sift_ctx* ctx, const float* d_img, int width, int height, size_t stride_px,
+                             const sift_params* p) {
+  if (!ctx) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->detect_pending) return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
+  return detect_enqueue(ctx, nullptr, d_img, width, height, stride_px, p);
+}
+
+int sift_detect_wait(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  return detect_finish(ctx, out, cap, n_out);
 }
 
 int sift_detect(sift_ctx* ctx, const float* img, int width, int height, size_t stride_px, const sift_params* p,

@@ -94,6 +94,11 @@ __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int
 
 template <int NP, int K>
 __device__ __forceinline__ void x_derive(XWin<NP>& Wn, const float (&src)[NP]) {
+#if defined(SIFT_X_PROBE) && SIFT_X_PROBE > 1  // timing probe: loads only
+#pragma unroll
+  for (int q = 0; q < NP; ++q) { Wn.hx[K][q] = src[q]; Wn.hn[K][q] = src[q]; }
+  return;
+#endif
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
     const float v = src[q];
@@ -112,6 +117,15 @@ __device__ __forceinline__ void x_derive(XWin<NP>& Wn, const float (&src)[NP]) {
 // Centre row y (slots A = y-1, B = y, C = y+1): decide every scale of the group.
 template <int NP, int A, int B, int C>
 __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const ExtremaLaunch& L, int y) {
+#if defined(SIFT_X_PROBE)  // timing probe: no decisions
+  {
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) acc += Wn.hx[B][q] + Wn.hn[A][q];
+    if (acc == 1234.5f) U.low += 1;
+    return;
+  }
+#endif
   float vx[NP], vn[NP];
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
@@ -124,33 +138,40 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     const float v = Wn.cv[B][q];
     const float nmax = max3f(vx[q - 1], vx[q + 1], max3f(Wn.hx[A][q], Wn.hx[C][q], Wn.ex[B][q]));
     const float nmin = min3f(vn[q - 1], vn[q + 1], min3f(Wn.hn[A][q], Wn.hn[C][q], Wn.en[B][q]));
-    const float av = __builtin_fabsf(v);
-    // Lane masks (SALU from here on).
-    const unsigned long long ge = __ballot(v >= nmax), le = __ballot(v <= nmin);
-    const unsigned long long gt = __ballot(v > nmax), lt = __ballot(v < nmin);
-    const unsigned long long lo = __ballot(av < L.c_lo), hi = __ballot(av >= L.c_hi);
-    const unsigned long long certain = (gt | lt) & U.colmask;
-    unsigned long long ext, tie;
-    if (L.exact_planes) { ext = certain; tie = 0ull; }
-    else { ext = (ge | le) & U.colmask; tie = ext & ~certain; }
-    const unsigned long long count_low = ext & lo & ~tie;
-    const unsigned long long bit = ext & ~count_low;
-    const unsigned long long amb = bit & (tie | ~hi);
-    U.low += (unsigned)__popcll(count_low);
-    const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
-    if (U.lane == q - 1) {
-      wlo = (unsigned)word;
-      whi = (unsigned)(word >> 32);
-      wcnt = (unsigned)__popcll(word);
-    }
-    if (amb) {  // rare: ties / contrast within fp32 rounding of the threshold
-      const bool mine = (amb >> U.lane) & 1ull;
-      const unsigned slot = wave_append(mine, &L.counters[0]);
-      if (mine && slot < L.amb_cap)
-        L.amb_keys[slot] = U.key_base + (unsigned)(q - 1) * (unsigned)U.plane + (unsigned)y * (unsigned)U.w +
-                           (unsigned)(U.xw * kXW - 1 + U.lane);
+    // Lane masks (SALU from here on).  Most rows of a 62-column word hold no
+    // extremum at a given scale: one ballot decides, the rest is skipped.
+    const unsigned long long ext_any = __ballot(v >= nmax || v <= nmin) & U.colmask;
+    if (ext_any) {
+      const float av = __builtin_fabsf(v);
+      const unsigned long long gt = __ballot(v > nmax), lt = __ballot(v < nmin);
+      const unsigned long long lo = __ballot(av < L.c_lo), hi = __ballot(av >= L.c_hi);
+      const unsigned long long certain = (gt | lt) & U.colmask;
+      unsigned long long ext, tie;
+      if (L.exact_planes) { ext = certain; tie = 0ull; }
+      else { ext = ext_any; tie = ext & ~certain; }
+      const unsigned long long count_low = ext & lo & ~tie;
+      const unsigned long long bit = ext & ~count_low;
+      const unsigned long long amb = bit & (tie | ~hi);
+      U.low += (unsigned)__popcll(count_low);
+      const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
+      if (U.lane == q - 1) {
+        wlo = (unsigned)word;
+        whi = (unsigned)(word >> 32);
+        wcnt = (unsigned)__popcll(word);
+      }
+      if (amb) {  // rare: ties / contrast within fp32 rounding of the threshold
+        const bool mine = (amb >> U.lane) & 1ull;
+        const unsigned slot = wave_append(mine, &L.counters[0]);
+        if (mine && slot < L.amb_cap)
+          L.amb_keys[slot] = U.key_base + (unsigned)(q - 1) * (unsigned)U.plane + (unsigned)y * (unsigned)U.w +
+                             (unsigned)(U.xw * kXW - 1 + U.lane);
+      }
     }
   }
+#if defined(SIFT_X_PROBE3)  // timing probe: decisions without bitmap stores
+  if (wlo == 0x12345u && whi == 0x777u) U.low += wcnt;
+  return;
+#endif
   if (U.lane < NP - 2) {
     const long long r = (long long)U.lane * U.h + y;
     U.bitmap[r * U.nw + U.xw] = ((unsigned long long)whi << 32) | wlo;
@@ -243,22 +264,27 @@ __global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaL
 // order at the row's offset.  Candidate values are the fp32 plane values
 // (ambiguous ones get their exact fp64 value from k_exact_extrema).
 __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch E) {
-  const Octave& oc = P.oct[E.o];
-  const int h = oc.h, w = oc.w;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // (s-1)*h + y
-  if (row >= P.S * h) return;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row
+  if (g >= E.row_off[E.n_oct]) return;
+  int o = 0;
+  while (o + 1 < E.n_oct && g >= E.row_off[o + 1]) ++o;
+  const Octave& oc = P.oct[o];
+  const int h = oc.h, w = oc.w;
+  const int row = g - E.row_off[o];  // (s-1)*h + y within the octave
   const int s = row / h + 1, y = row - (s - 1) * h;
   if (y < 1 || y > h - 2) return;
-  const unsigned cnt = E.rowcount[row];
+  const unsigned cnt = E.rowcount[g];
   if (cnt == 0) return;
-  unsigned base = E.rowoff[E.row_base + row];
+  unsigned base = E.rowoff[g];
   const long long plane = (long long)h * w;
   const float* __restrict__ Dc = P.dog + oc.dog_off + s * plane + (long long)y * w;
   const unsigned kbase = oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w;
-  for (int xw0 = 0; xw0 < E.nw; xw0 += 64) {
+  const int nw = E.nw[o];
+  const unsigned long long* bm = E.bitmap + E.word_off[o] + (long long)row * nw;
+  for (int xw0 = 0; xw0 < nw; xw0 += 64) {
     const int xw = xw0 + lane;
-    unsigned long long word = xw < E.nw ? E.bitmap[(long long)row * E.nw + xw] : 0ull;
+    unsigned long long word = xw < nw ? bm[xw] : 0ull;
     unsigned c = (unsigned)__popcll(word);
     // inclusive wave scan of c
     unsigned inc = c;
@@ -346,9 +372,8 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
 }
 
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st) {
-  const Octave& oc = P.oct[E.o];
-  if (oc.h < 3 || oc.w < 3) return hipSuccess;
-  const int rows = P.S * oc.h;
+  const int rows = E.row_off[E.n_oct];
+  if (rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_emit, dim3((rows + 3) / 4), dim3(256), 0, st, P, E);
   return hipGetLastError();
 }

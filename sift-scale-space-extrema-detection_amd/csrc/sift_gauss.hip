@@ -270,57 +270,70 @@ __device__ __forceinline__ void vert_o0(const GTile& T, const cdouble* wp, doubl
 template <int R>
 __device__ __forceinline__ void horz_full(const GTile& T, const cdouble* wp, const double* V,
                                           double (&out)[kNR][4]) {
+  // Both rows of the lane in one loop: 8 independent fma chains per wave
+  // (4 leave the fp64 pipeline latency exposed).
   constexpr int NP = R + 2;  // double2 pairs per row
+  const double* rp[kNR];
+  double2 u[kNR][NP];
 #pragma unroll
   for (int i = 0; i < kNR; ++i) {
-    const double* rp = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 4 * T.cg;
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    double2 u[NP];
+    rp[i] = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 4 * T.cg;
 #pragma unroll
-    for (int n2 = 0; n2 < kPFH && n2 < NP; ++n2) u[n2] = *reinterpret_cast<const double2*>(rp + 2 * n2);
+    for (int q = 0; q < 4; ++q) out[i][q] = 0.0;
+  }
 #pragma unroll
-    for (int n2 = 0; n2 < NP; ++n2) {
-      if (n2 + kPFH < NP) u[n2 + kPFH] = *reinterpret_cast<const double2*>(rp + 2 * (n2 + kPFH));
+  for (int n2 = 0; n2 < kPFH && n2 < NP; ++n2)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int n = 2 * n2 + e;
-        const double v = e ? u[n2].y : u[n2].x;
+    for (int i = 0; i < kNR; ++i) u[i][n2] = *reinterpret_cast<const double2*>(rp[i] + 2 * n2);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int k = n - q;
-          if (k >= 0 && k <= 2 * R) a[q] = fma((double)wp[k], v, a[q]);
-        }
+  for (int n2 = 0; n2 < NP; ++n2) {
+    if (n2 + kPFH < NP)
+#pragma unroll
+      for (int i = 0; i < kNR; ++i) u[i][n2 + kPFH] = *reinterpret_cast<const double2*>(rp[i] + 2 * (n2 + kPFH));
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * n2 + e;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = n - q;
+        if (k >= 0 && k <= 2 * R)
+#pragma unroll
+          for (int i = 0; i < kNR; ++i) out[i][q] = fma((double)wp[k], e ? u[i][n2].y : u[i][n2].x, out[i][q]);
       }
-      pin(a);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[i][q] = a[q];
+    for (int i = 0; i < kNR; ++i) pin(out[i]);
   }
 }
 
 __device__ __forceinline__ void horz_full_gen(const GTile& T, int r, const cdouble* wp, const double* V,
                                               double (&out)[kNR][4]) {
   const int NV = 2 * r + 4;
+  const double* rp[kNR];
 #pragma unroll
   for (int i = 0; i < kNR; ++i) {
-    const double* rp = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 4 * T.cg;
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int nb = 0; nb < NV; nb += 8) {
-      double u[8];
+    rp[i] = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 4 * T.cg;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[i][q] = 0.0;
+  }
+  for (int nb = 0; nb < NV; nb += 8) {
+    double u[kNR][8];
+#pragma unroll
+    for (int i = 0; i < kNR; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const double2 p = *reinterpret_cast<const double2*>(rp + nb + 2 * e);
-        u[2 * e] = p.x;
-        u[2 * e + 1] = p.y;
+        const double2 p = *reinterpret_cast<const double2*>(rp[i] + nb + 2 * e);
+        u[i][2 * e] = p.x;
+        u[i][2 * e + 1] = p.y;
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
+    for (int e = 0; e < 8; ++e)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] = fma((double)wp[nb + e - q], u[e], a[q]);  // zero-padded taps
-      pin(a);
-    }
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[i][q] = a[q];
+        for (int i = 0; i < kNR; ++i) out[i][q] = fma((double)wp[nb + e - q], u[i][e], out[i][q]);  // zero-padded taps
+#pragma unroll
+    for (int i = 0; i < kNR; ++i) pin(out[i]);
   }
 }
 
@@ -331,33 +344,39 @@ __device__ __forceinline__ void horz_o0(const GTile& T, const cdouble* wp, const
                                         double (&out)[kNR][4]) {
   constexpr int HR = cl2(R);
   constexpr int NP = (fl2(R + 3) + HR + 2) / 2;  // double2 pairs per row
+  const double* rp[kNR];
+  double2 u[kNR][NP];
 #pragma unroll
   for (int i = 0; i < kNR; ++i) {
-    const double* rp = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 2 * T.cg;
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    double2 u[NP];
+    rp[i] = V + (8 * T.wv + T.rs + kRS * i) * T.sw + 2 * T.cg;
 #pragma unroll
-    for (int n2 = 0; n2 < kPFH && n2 < NP; ++n2) u[n2] = *reinterpret_cast<const double2*>(rp + 2 * n2);
+    for (int q = 0; q < 4; ++q) out[i][q] = 0.0;
+  }
 #pragma unroll
-    for (int n2 = 0; n2 < NP; ++n2) {
-      if (n2 + kPFH < NP) u[n2 + kPFH] = *reinterpret_cast<const double2*>(rp + 2 * (n2 + kPFH));
+  for (int n2 = 0; n2 < kPFH && n2 < NP; ++n2)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int n = 2 * n2 + e;
-        const double v = e ? u[n2].y : u[n2].x;
+    for (int i = 0; i < kNR; ++i) u[i][n2] = *reinterpret_cast<const double2*>(rp[i] + 2 * n2);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+  for (int n2 = 0; n2 < NP; ++n2) {
+    if (n2 + kPFH < NP)
 #pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const int k = 2 * (n - HR) + R - q + d;
-            if (k >= 0 && k <= 2 * R) a[q] = fma((double)wp[k], v, a[q]);
-          }
+      for (int i = 0; i < kNR; ++i) u[i][n2 + kPFH] = *reinterpret_cast<const double2*>(rp[i] + 2 * (n2 + kPFH));
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * n2 + e;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const int k = 2 * (n - HR) + R - q + d;
+          if (k >= 0 && k <= 2 * R)
+#pragma unroll
+            for (int i = 0; i < kNR; ++i) out[i][q] = fma((double)wp[k], e ? u[i][n2].y : u[i][n2].x, out[i][q]);
         }
       }
-      pin(a);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[i][q] = a[q];
+    for (int i = 0; i < kNR; ++i) pin(out[i]);
   }
 }
 
@@ -481,10 +500,15 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   double lprev[kNR][4];
   for (int s = s_first; s < s_end; ++s) {
     const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
-    vert_any<OCT0, RMAX>(T, oc.rad[s], wp, V);
+    // Per-lane indices made opaque each scale: otherwise the compiler hoists
+    // every radius variant's address arithmetic out of the scale loop and
+    // keeps it all live (dozens of VGPRs, half the occupancy).
+    GTile Ts = T;
+    asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
+    vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
     wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
     double out[kNR][4];
-    horz_any<OCT0, RMAX>(T, oc.rad[s], wp, V, out);
+    horz_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V, out);
     wave_lds_fence();  // strip rows read before the next scale overwrites them
 
     if (s >= s_begin && (st || out[0][0] == 12345.0)) {

@@ -49,13 +49,16 @@ struct ExtremaLaunch {
   unsigned amb_cap;
 };
 
+// One launch over every octave: global row g (one wave each) = row_off[o] +
+// (s-1) h_o + y.
 struct EmitLaunch {
-  int o;
+  int n_oct;
+  int row_off[kMaxOctaves + 1];  // first global row of each octave ([S][h] rows per octave)
+  long long word_off[kMaxOctaves];  // first bitmap word of each octave
+  int nw[kMaxOctaves];
   const unsigned long long* bitmap;
-  int nw;
-  const unsigned* rowcount;      // this octave's [S][h]
-  const unsigned* rowoff;        // exclusive scan over all octaves' row counts
-  int row_base;                  // index of this octave's first row in rowoff
+  const unsigned* rowcount;      // [all rows]
+  const unsigned* rowoff;        // exclusive scan of rowcount
   unsigned* keys;                // ordered candidate keys
   double* value;
   unsigned* keep;

@@ -52,6 +52,12 @@ struct StepOut {
 // and each bound gets a factor kSafe of slack.  A decision inside its bound
 // sets `uncertain`.  On the last iteration (`last`) a move discards, so the
 // new position's rounding does not matter.
+// APPROX (fast pass on fp32 planes only): the inverse uses one reciprocal
+// instead of nine divisions.  Its extra rounding (~1e-16 relative) is far
+// inside the fp32-plane error bounds every decision already carries; the
+// exact pass and caller-supplied planes (delta == 0) keep the reference's
+// divisions.
+template <bool APPROX>
 __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int n, double value,
                                       double delta, double dval, int S, int ND, int h, int w,
                                       double thr, bool last) {
@@ -102,13 +108,14 @@ __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int 
   }
   double ninv[3][3];
   double inv_norm = 0;
+  const double rdet = APPROX ? 1.0 / det : 0.0;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     double rs = 0;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const double cof = ((i + j) & 1) ? mn[j][i] * -1.0 : mn[j][i];
-      ninv[i][j] = (cof / det) * -1;
+      ninv[i][j] = (APPROX ? cof * rdet : cof / det) * -1;
       rs += fabs(ninv[i][j]);
     }
     inv_norm = fmax(inv_norm, rs);
@@ -236,7 +243,9 @@ __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const Refi
           }
       // fp32 rounding of the fp64 value (<= |v| 2^-24) plus fp64 noise vs the reference.
       const double delta = L.exact_planes ? 0.0 : mx * (0x1p-24 + 0x1p-40);
-      const StepOut R = refine_step(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4);
+      const StepOut R = L.exact_planes
+                            ? refine_step<false>(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4)
+                            : refine_step<true>(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4);
       if (R.uncertain) {
         unc = true;
         for (int b = 0; b < 6; ++b)
@@ -287,7 +296,7 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
       wave_dog_patch(P, o, s, m, n, sh, Lbuf, d27);
       if (threadIdx.x == 0) {
         if (it == 0) value = d27[13];  // exact fp64 candidate value (:565 uses it)
-        const StepOut R = refine_step(d27, o, s, m, n, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr, it == 4);
+        const StepOut R = refine_step<false>(d27, o, s, m, n, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr, it == 4);
         int cont = 0;
         if (R.state == 3) status = kRefSingular;
         else if (R.state == 2) status = kRefDiscard;

@@ -37,6 +37,7 @@ ABI_SYMBOLS = (
     "sift_set_candidates", "sift_refine_params", "sift_copy_candidates", "sift_copy_keypoints",
     "sift_copy_keypoints_device", "sift_detect", "sift_detect_device", "sift_last_counts",
     "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
+    "sift_detect_device_async", "sift_detect_wait", "sift_ctx_create_shared",
 )
 
 
@@ -126,6 +127,9 @@ def lib():
         "sift_copy_keypoints_device": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_detect": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_detect_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
+        "sift_detect_device_async": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp]),
+        "sift_detect_wait": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_ctx_create_shared": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
         "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
         "sift_last_timings": (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
         "sift_device_keypoints": (ctypes.c_int, [vp, ctypes.POINTER(vp), szp]),
@@ -170,12 +174,18 @@ def octave_dims(width, height, num_octaves):
 class Context:
     """One sift_ctx: a HIP stream plus device-resident pyramids on `device`."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, share=None):
+        """share: another Context whose HIP stream this one uses (its work is
+        ordered after the other's; keep `share` open longer than this one)."""
         self._L = lib()
         h = ctypes.c_void_p()
-        rc = self._L.sift_ctx_create(int(device), ctypes.byref(h))
+        if share is not None:
+            rc = self._L.sift_ctx_create_shared(share._h, ctypes.byref(h))
+        else:
+            rc = self._L.sift_ctx_create(int(device), ctypes.byref(h))
         if rc:
             raise SiftError(rc, "sift_ctx_create(device=%d) failed (no HIP device?)" % device)
+        self._share = share  # keeps the stream owner alive
         self._h = h
         self.params = None
         self.width = self.height = 0
@@ -316,6 +326,23 @@ class Context:
             rc = SIFT_OK
         self._check(rc, "sift_detect_device")
         self.params, self.width, self.height = params, width, height
+        return n.value
+
+    def detect_device_async(self, d_ptr, width, height, params, stride=None):
+        """Enqueue one detection and return (sift_detect_device_async); finish
+        with detect_wait().  One in flight per context."""
+        self._check(self._L.sift_detect_device_async(self._h, ctypes.c_void_p(int(d_ptr)), int(width), int(height),
+                                                     int(stride or width), ctypes.byref(params)),
+                    "sift_detect_device_async")
+        self.params, self.width, self.height = params, width, height
+
+    def detect_wait(self, raise_singular=False):
+        """Complete the detection in flight; returns the keypoint count."""
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect_wait(self._h, None, 0, ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect_wait")
         return n.value
 
     def device_keypoints(self):

@@ -215,3 +215,34 @@ def test_unaligned_widths_match_oracle(gpu_ctx, W, H):
     r = orc.OracleRun(img, _oracle_params(p), orc.CONV_SEPARABLE)
     check_candidates(gpu_ctx.candidates(), r.candidates())
     check_keypoints(kp, r.refined)
+
+
+def _device_copy(img):
+    """hipMalloc + upload through the HIP runtime libsift_hip.so uses (torch may
+    bundle a different one, which must not share the process's device state)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ptr = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(img.nbytes)) == 0
+    assert hip.hipMemcpy(ptr, img.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(img.nbytes), 1) == 0  # H2D
+    return hip, ptr
+
+
+def test_async_detect_matches_sync():
+    """sift_detect_device_async / sift_detect_wait on two contexts in flight
+    give the same keypoints as the synchronous call."""
+    img = np.ascontiguousarray(blob_image(640, 360, seed=41), dtype=np.float32)
+    p = sift_amd.make_params(4, 4)
+    hip, d = _device_copy(img)
+    try:
+        with sift_amd.Context(0) as a, sift_amd.Context(0, share=a) as b, sift_amd.Context(0) as c:
+            n_ref = c.detect_device(d.value, 640, 360, p)
+            ref = c.keypoints().tobytes()
+            a.detect_device_async(d.value, 640, 360, p)
+            b.detect_device_async(d.value, 640, 360, p)
+            with pytest.raises(sift_amd.SiftError):
+                a.detect_device_async(d.value, 640, 360, p)  # one in flight per context
+            assert a.detect_wait() == n_ref and b.detect_wait() == n_ref
+            assert a.keypoints().tobytes() == ref and b.keypoints().tobytes() == ref
+    finally:
+        hip.hipFree(d)

@@ -1,0 +1,6 @@
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+export TMPDIR=/tmp SIFT_HIP_LIB=$R/build_var/h8.so
+cd /tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_FMA_F32 --output-format csv -d $O/pmc_cls -o run -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $O/pmc_cls.err || { tail -3 $O/pmc_cls.err; exit 1; }
+echo ok
