@@ -1029,8 +1029,9 @@ int sift_copy_keypoints_device(sift_ctx* ctx, void* d_dst, size_t cap, size_t* n
   if (cap < ctx->n_kp) return set_err(ctx, SIFT_E_CAPACITY, "keypoint buffer too small");
   if (ctx->n_kp) {
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipMemcpyAsync(d_dst, ctx->kp.p, ctx->n_kp * sizeof(sift_keypoint), hipMemcpyDeviceToDevice, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // The keypoints are final (the detection was waited for): copy off the
+    // context stream, so a detection queued behind them is not waited for.
+    HIPCHK(hipMemcpy(d_dst, ctx->kp.p, ctx->n_kp * sizeof(sift_keypoint), hipMemcpyDeviceToDevice));
   }
   return SIFT_OK;
 }
