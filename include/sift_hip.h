@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 2
+#define SIFT_ABI_VERSION 3
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -55,7 +55,9 @@ enum { SIFT_PLANE_GAUSS = 0, SIFT_PLANE_DOG = 1 };
 /* sift_params.flags */
 enum {
   SIFT_F_SKIP_GAUSS_PLANES = 1 << 0, /* do not materialise Gaussian planes (seeds still kept) */
-  SIFT_F_SKIP_DOG_PLANES = 1 << 1    /* reserved: DoG planes are needed by refinement today   */
+  SIFT_F_SKIP_DOG_PLANES = 1 << 1,   /* reserved: DoG planes are needed by refinement today   */
+  SIFT_F_EXPORT_NEXT_SEED = 1 << 2,  /* also form the fp64 base of octave num_octaves (sift_next_seed) */
+  SIFT_F_KEYPOINT_ORIGINS = 1 << 3   /* record each keypoint's candidate (sift_keypoint_origins) */
 };
 
 /* Parameters of the pipeline.  Names and defaults follow
@@ -216,6 +218,44 @@ int sift_copy_keypoints_device(struct sift_ctx *ctx, void *d_dst, size_t cap, si
  * the RCCL all-gather of keypoints).  Valid until the next build/detect. */
 int sift_device_keypoints(struct sift_ctx *ctx, const sift_keypoint **d_kp, size_t *n);
 void *sift_stream(struct sift_ctx *ctx);
+
+/* Row-band sharding of one image over several devices (ABI version >= 3;
+ * SURVEY.md §8e cfg 5, no reference counterpart: the reference is one Web
+ * Worker).  A shard runs the leading octaves on a crop of whole input rows
+ * (sift_detect with num_octaves = K + 1, SIFT_F_EXPORT_NEXT_SEED and
+ * SIFT_F_KEYPOINT_ORIGINS), keeps the keypoints whose candidate row it owns
+ * and contributes its owned rows of the octave-(K+1) base; the base rows of
+ * all shards make the whole base, from which sift_detect_from_seed runs the
+ * trailing octaves.  The pipeline is translation invariant in y, so rows far
+ * enough from a crop edge are bit-identical to the whole-image run. */
+
+/* Input row of the first row of the images given to the following builds /
+ * detections (a crop of whole rows of a taller image; default 0): keypoint
+ * local_y / abs_y and origins are reported in the whole image's rows.  The
+ * crop's first row must be a multiple of 2^(num_octaves - 1) (octave rows
+ * stay whole). */
+int sift_set_row_origin(struct sift_ctx *ctx, int input_row0);
+
+/* The fp64 base of octave num_octaves formed by the last build with
+ * SIFT_F_EXPORT_NEXT_SEED: rows x cols, row-major (host copy / device
+ * pointer valid until the next build). */
+int sift_next_seed(struct sift_ctx *ctx, double *dst, size_t cap, int *rows, int *cols);
+int sift_device_next_seed(struct sift_ctx *ctx, const double **d_seed, int *rows, int *cols);
+
+/* Detection of octaves octave_first .. num_octaves-1 of a width x height
+ * input from the fp64 base of octave octave_first (>= 1; rows x cols as
+ * sift_octave_dims gives, row-major, host or device memory).  Octave
+ * indices, scales and absolute coordinates are those of the whole-image run. */
+int sift_detect_from_seed(struct sift_ctx *ctx, int octave_first, const double *seed, int width, int height,
+                          const sift_params *p, sift_keypoint *out, size_t cap, size_t *n_out);
+int sift_detect_from_seed_device(struct sift_ctx *ctx, int octave_first, const double *d_seed, int width,
+                                 int height, const sift_params *p, sift_keypoint *out, size_t cap,
+                                 size_t *n_out);
+
+/* The candidate (octave, scale, y, x) of each keypoint of the last
+ * detection/refinement run with SIFT_F_KEYPOINT_ORIGINS: 4 int32 per
+ * keypoint, keypoint order (the reference's candidate order). */
+int sift_keypoint_origins(struct sift_ctx *ctx, int32_t *out, size_t cap, size_t *n_out);
 
 /* Wait for all work queued on ctx's stream. */
 int sift_synchronize(struct sift_ctx *ctx);

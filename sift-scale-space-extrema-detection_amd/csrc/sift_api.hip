@@ -77,6 +77,11 @@ struct sift_ctx {
   bool detect_pending = false;   // sift_detect_device_async enqueued, sift_detect_wait not yet called
   bool detect_host_img = false;
   ExtremaLaunch xl{};       // extrema launch state between prepare / scan / finish
+  int o_first = 0;          // first octave of the pyramid in use (sift_detect_from_seed: > 0)
+  int row0 = 0;             // sift_set_row_origin: input row of the image's first row
+  int xseed_h = 0, xseed_w = 0;  // SIFT_F_EXPORT_NEXT_SEED: the base of octave O
+  bool has_xseed = false;
+  bool has_origins = false; // kp_key holds the candidate key of every keypoint
   std::vector<long long> x_word_off, x_row_off;
   long long x_rows = 0;
   // device memory
@@ -87,6 +92,7 @@ struct sift_ctx {
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
   DBuf keep, pos;                              // keypoint compaction
   DBuf status, kp_tmp, kp, uncertain;          // refinement
+  DBuf xseed, kp_key;                          // next-octave base, keypoint origins
   DBuf counters, temp;
   unsigned* h_counters = nullptr;              // pinned mirror of counters
   hipEvent_t ev[8]{};
@@ -216,7 +222,8 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
-                  &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->counters, &ctx->temp};
+                  &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->xseed, &ctx->kp_key, &ctx->counters,
+                  &ctx->temp};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -269,6 +276,7 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
   P.W = W; P.H = H;
   const double thr = ((std::pow(2.0, 1.0 / S) - 1) / (std::pow(2.0, 1.0 / 3) - 1)) * 0.015;
   P.thr = thr;             // background.js:572
+  P.row0 = ctx->row0;
   P.pix_thr = thr * 0.8;   // sift.js:285-294
   std::vector<double> w;
   long long goff = 0, doff = 0, soff = 0;
@@ -346,15 +354,22 @@ static int extrema_scan(sift_ctx* ctx, int o0, int o1, hipStream_t st);
 // overlap_extrema: launch each octave's extrema scan on the side stream as
 // soon as its DoG planes exist, overlapping the next octaves' Gaussian
 // kernels (memory-bound scans beside FMA-bound small octaves).
+// o_first > 0 (sift_detect_from_seed): no image; the fp64 base of octave
+// o_first is seed_host / seed_dev and octaves o_first .. O-1 are built.
 static int build_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
-                        size_t stride, const sift_params* p, const double* sig, bool overlap_extrema = false) {
+                        size_t stride, const sift_params* p, const double* sig, bool overlap_extrema = false,
+                        int o_first = 0, const double* seed_host = nullptr, const double* seed_dev = nullptr) {
   if (!ctx) return SIFT_E_ARG;
-  if (!img_host && !img_dev) return set_err(ctx, SIFT_E_ARG, "null image");
-  if (stride < (size_t)W) return set_err(ctx, SIFT_E_ARG, "stride < width");
+  if (o_first == 0 && !img_host && !img_dev) return set_err(ctx, SIFT_E_ARG, "null image");
+  if (o_first > 0 && !seed_host && !seed_dev) return set_err(ctx, SIFT_E_ARG, "null seed");
+  if (o_first == 0 && stride < (size_t)W) return set_err(ctx, SIFT_E_ARG, "stride < width");
   HIPCHK(hipSetDevice(ctx->device));
   int rc = setup_geometry(ctx, W, H, p, sig, true);
   if (rc) return rc;
   Pyramid& P = ctx->P;
+  if (o_first < 0 || o_first >= P.O) return set_err(ctx, SIFT_E_ARG, "octave_first out of range");
+  ctx->o_first = o_first;
+  ctx->has_xseed = false;
   const long long tot = total_plane_px(ctx);
   const bool keep_gauss = !(p->flags & SIFT_F_SKIP_GAUSS_PLANES);
   HIPCHK(ctx->dog.ensure((size_t)tot * P.ND * sizeof(float)));
@@ -362,7 +377,14 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   HIPCHK(ctx->seeds.ensure((size_t)std::max<long long>(1, tot - (long long)P.oct[0].h * P.oct[0].w) *
                            sizeof(double)));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
-  if (img_host) {
+  if (o_first > 0) {
+    const Octave& of = P.oct[o_first];
+    HIPCHK(hipMemcpyAsync(ctx->seeds.as<double>() + of.seed_off, seed_host ? (const void*)seed_host : seed_dev,
+                          (size_t)of.h * of.w * sizeof(double),
+                          seed_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, ctx->stream));
+    P.img = nullptr;
+    P.img_stride = 0;
+  } else if (img_host) {
     HIPCHK(ctx->img.ensure((size_t)W * H * sizeof(float)));
     HIPCHK(hipMemcpy2DAsync(ctx->img.p, W * sizeof(float), img_host, stride * sizeof(float),
                             W * sizeof(float), H, hipMemcpyHostToDevice, ctx->stream));
@@ -376,7 +398,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   P.dog = ctx->dog.as<float>();
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   const double* base0 = nullptr;
-  if (gauss_needs_base0(P)) {
+  if (o_first == 0 && gauss_needs_base0(P)) {
     HIPCHK(ctx->base0.ensure((size_t)P.oct[0].h * P.oct[0].w * sizeof(double)));
     HIPCHK(launch_upsample_base(P, ctx->base0.as<double>(), ctx->stream));
     base0 = ctx->base0.as<double>();
@@ -390,17 +412,24 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     rc = extrema_prepare(ctx, ctx->side);
     if (rc) return rc;
   }
-  for (int o = 0; o < P.O; ++o) {
+  const bool xseed = (p->flags & SIFT_F_EXPORT_NEXT_SEED) != 0;
+  if (xseed) {
+    ctx->xseed_h = (P.oct[P.O - 1].h + 1) / 2;  // background.js:118
+    ctx->xseed_w = (P.oct[P.O - 1].w + 1) / 2;
+    HIPCHK(ctx->xseed.ensure((size_t)ctx->xseed_h * ctx->xseed_w * sizeof(double)));
+  }
+  for (int o = o_first; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
     GaussLaunch L{};
     L.o = o;
     L.base = o == 0 ? base0 : ctx->seeds.as<double>() + oc.seed_off;
     L.gauss = keep_gauss ? ctx->gauss.as<float>() + oc.gauss_off : nullptr;
     L.dog = ctx->dog.as<float>() + oc.dog_off;
-    L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off : nullptr;
-    L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : 0;
+    L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off
+                                : (xseed ? ctx->xseed.as<double>() : nullptr);
+    L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : (xseed ? ctx->xseed_w : 0);
     HIPCHK(launch_gauss_dog(P, L, ctx->stream));
-    if (o == 0) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+    if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     if (overlap) {
       HIPCHK(hipEventRecord(ctx->ev_oct[o], ctx->stream));
       HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_oct[o], 0));
@@ -418,6 +447,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   ctx->dog_source = kNative;
   ctx->have_gauss = keep_gauss;
   ctx->have_cand = false;
+  ctx->has_xseed = xseed;
   return SIFT_OK;
 }
 
@@ -474,6 +504,7 @@ int sift_get_plane(sift_ctx* ctx, int kind, int o, int s, float* dst, size_t cap
   if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no pyramid");
   const Pyramid& P = ctx->P;
   if (o < 0 || o >= P.O) return set_err(ctx, SIFT_E_ARG, "octave out of range");
+  if (o < ctx->o_first) return set_err(ctx, SIFT_E_STATE, "octave not built (sift_detect_from_seed)");
   const Octave& oc = P.oct[o];
   const size_t plane = (size_t)oc.h * oc.w;
   if (cap_px < plane) return set_err(ctx, SIFT_E_CAPACITY, "destination too small");
@@ -507,6 +538,7 @@ int sift_load_dog(sift_ctx* ctx, const float* planes, int width, int height, con
   ctx->P.img = nullptr;
   ctx->P.seeds = nullptr;
   ctx->dog_source = kForeign;
+  ctx->o_first = 0;
   ctx->have_gauss = false;
   ctx->have_cand = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -534,6 +566,7 @@ int sift_load_scale_space(sift_ctx* ctx, const float* planes, int width, int hei
   ctx->P.img = nullptr;
   ctx->P.seeds = nullptr;
   ctx->dog_source = kForeign;
+  ctx->o_first = 0;
   ctx->have_gauss = true;
   ctx->have_cand = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -677,7 +710,7 @@ static int launch_extrema_stage(sift_ctx* ctx) {
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   int rc = extrema_prepare(ctx, ctx->stream);
   if (rc) return rc;
-  rc = extrema_scan(ctx, 0, ctx->P.O, ctx->stream);
+  rc = extrema_scan(ctx, ctx->o_first, ctx->P.O, ctx->stream);
   if (rc) return rc;
   return extrema_finish(ctx);
 }
@@ -763,7 +796,13 @@ static int refine_enqueue(sift_ctx* ctx) {
     HIPCHK(launch_scatter_keypoints(R.status, ctx->pos.as<unsigned>(), R.kp, R.n, cap, ctx->kp.as<Keypoint>(),
                                     ctx->stream));
     HIPCHK(launch_count_keypoints(ctx->pos.as<unsigned>(), ctx->keep.as<unsigned>(), R.n, cap, cnt + kCntKp, ctx->stream));
+    if (ctx->p.flags & SIFT_F_KEYPOINT_ORIGINS) {
+      HIPCHK(ctx->kp_key.ensure((size_t)cap * sizeof(unsigned)));
+      HIPCHK(launch_scatter_keys(R.status, ctx->pos.as<unsigned>(), R.cand_key, R.n, cap, ctx->kp_key.as<unsigned>(),
+                                 ctx->stream));
+    }
   }
+  ctx->has_origins = (ctx->p.flags & SIFT_F_KEYPOINT_ORIGINS) != 0;
   HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 32 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->stream));
   return SIFT_OK;
@@ -1040,6 +1079,87 @@ int sift_device_keypoints(sift_ctx* ctx, const sift_keypoint** d_kp, size_t* n) 
   if (!ctx || !d_kp || !n) return SIFT_E_ARG;
   *d_kp = ctx->kp.as<const sift_keypoint>();
   *n = ctx->n_kp;
+  return SIFT_OK;
+}
+
+int sift_device_next_seed(sift_ctx* ctx, const double** d_seed, int* rows, int* cols) {
+  if (!ctx || !d_seed) return SIFT_E_ARG;
+  if (!ctx->has_xseed) return set_err(ctx, SIFT_E_STATE, "no next-octave base (SIFT_F_EXPORT_NEXT_SEED)");
+  *d_seed = ctx->xseed.as<const double>();
+  if (rows) *rows = ctx->xseed_h;
+  if (cols) *cols = ctx->xseed_w;
+  return SIFT_OK;
+}
+
+int sift_next_seed(sift_ctx* ctx, double* dst, size_t cap, int* rows, int* cols) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->has_xseed) return set_err(ctx, SIFT_E_STATE, "no next-octave base (SIFT_F_EXPORT_NEXT_SEED)");
+  if (rows) *rows = ctx->xseed_h;
+  if (cols) *cols = ctx->xseed_w;
+  if (!dst) return SIFT_OK;
+  const size_t n = (size_t)ctx->xseed_h * ctx->xseed_w;
+  if (cap < n) return set_err(ctx, SIFT_E_CAPACITY, "destination too small");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(dst, ctx->xseed.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+static int detect_from_seed(sift_ctx* ctx, int o_first, const double* seed_host, const double* seed_dev, int W,
+                            int H, const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
+  if (!ctx || !p) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->detect_pending) return set_err(ctx, SIFT_E_STATE, "a detection is in flight on this context");
+  if (o_first < 1) return set_err(ctx, SIFT_E_ARG, "octave_first must be >= 1");
+  int rc = build_common(ctx, nullptr, nullptr, W, H, 0, p, nullptr, false, o_first, seed_host, seed_dev);
+  if (rc) return rc;
+  rc = launch_extrema_stage(ctx);
+  if (rc) return rc;
+  rc = refine_enqueue(ctx);
+  if (rc) return rc;
+  ctx->detect_pending = true;
+  ctx->detect_host_img = false;
+  return detect_finish(ctx, out, cap, n_out);
+}
+
+int sift_detect_from_seed(sift_ctx* ctx, int octave_first, const double* seed, int width, int height,
+                          const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
+  return detect_from_seed(ctx, octave_first, seed, nullptr, width, height, p, out, cap, n_out);
+}
+
+int sift_detect_from_seed_device(sift_ctx* ctx, int octave_first, const double* d_seed, int width, int height,
+                                 const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
+  return detect_from_seed(ctx, octave_first, nullptr, d_seed, width, height, p, out, cap, n_out);
+}
+
+int sift_set_row_origin(sift_ctx* ctx, int input_row0) {
+  if (!ctx || input_row0 < 0) return SIFT_E_ARG;
+  ctx->row0 = input_row0;
+  return SIFT_OK;
+}
+
+int sift_keypoint_origins(sift_ctx* ctx, int32_t* out, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->has_origins) return set_err(ctx, SIFT_E_STATE, "no keypoint origins (SIFT_F_KEYPOINT_ORIGINS)");
+  if (n_out) *n_out = ctx->n_kp;
+  if (!out || ctx->n_kp == 0) return SIFT_OK;
+  if (cap < 4 * ctx->n_kp) return set_err(ctx, SIFT_E_CAPACITY, "destination too small (4 per keypoint)");
+  HIPCHK(hipSetDevice(ctx->device));
+  std::vector<unsigned> keys(ctx->n_kp);
+  HIPCHK(hipMemcpyAsync(keys.data(), ctx->kp_key.p, keys.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const Pyramid& P = ctx->P;
+  for (size_t i = 0; i < keys.size(); ++i) {  // key = key_off(o) + (s-1) h w + y w + x
+    int o = P.O - 1;
+    while (o > 0 && keys[i] < P.oct[o].key_off) --o;
+    const Octave& oc = P.oct[o];
+    const unsigned plane = (unsigned)oc.h * (unsigned)oc.w, r = keys[i] - oc.key_off;
+    out[4 * i + 0] = o;
+    out[4 * i + 1] = (int32_t)(r / plane) + 1;
+    out[4 * i + 2] = (int32_t)((r % plane) / (unsigned)oc.w) + ((P.row0 * 2) >> o);
+    out[4 * i + 3] = (int32_t)((r % plane) % (unsigned)oc.w);
+  }
   return SIFT_OK;
 }
 

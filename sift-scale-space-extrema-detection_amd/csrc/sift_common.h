@@ -41,6 +41,7 @@ struct Pyramid {
   const float* dog;
   double pix_thr;        // 0.8 * thr   (sift.js:285-294)
   double thr;            // thr         (background.js:572)
+  int row0;              // input row of the input's first row (a row-band crop; 0 = whole image)
   Octave oct[kMaxOctaves];
 };
 

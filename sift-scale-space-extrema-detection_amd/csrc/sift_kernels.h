@@ -116,6 +116,8 @@ hipError_t launch_scatter_keypoints(const int* status, const unsigned* pos, cons
                                     const unsigned* n, int cap, Keypoint* out, hipStream_t st);
 hipError_t launch_status_to_keep(const int* status, unsigned* keep, const unsigned* n, int cap,
                                  hipStream_t st);
+hipError_t launch_scatter_keys(const int* status, const unsigned* pos, const unsigned* key, const unsigned* n,
+                               int cap, unsigned* out, hipStream_t st);
 // out = pos[n-1] + keep[n-1] (0 if n == 0): the number of keypoints.
 hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, const unsigned* n, int cap,
                                   unsigned* out, hipStream_t st);

@@ -199,14 +199,17 @@ __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int 
   return R;
 }
 
+// moff: octave-row offset of a row-band crop (P.row0 in octave-o rows), so
+// local_y and abs_y are those of the whole image: delta (a1 + m) with the
+// image row m, the reference's own rounding.
 __device__ inline void make_keypoint(Keypoint& k, int o, const StepOut& R, int S, double min_blur,
-                                     double mid) {
+                                     double mid, int moff) {
   const double delta = ldexp(1.0, o - 1);  // Math.pow(2, octave - 1), exact
   k.octave = o;
   k.scale_level = R.s;
   k.local_x = R.n;
-  k.local_y = R.m;
-  k.abs_y = delta * (R.a[1] + R.m);
+  k.local_y = R.m + moff;
+  k.abs_y = delta * (R.a[1] + (R.m + moff));
   k.abs_x = delta * (R.a[2] + R.n);
   k.abs_sigma = (delta / mid) * min_blur * pow(2.0, (R.a[0] + R.s) / S);
   k.interp_value = R.omega;
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const Refi
       if (R.state == 2) { status = kRefDiscard; break; }
       if (R.state == 1) {
         status = kRefKeep;
-        make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance);
+        make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance, (P.row0 * 2) >> o);
         break;
       }
       s = R.s; m = R.m; n = R.n;
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
         else if (R.state == 2) status = kRefDiscard;
         else if (R.state == 1) {
           status = kRefKeep;
-          make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance);
+          make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance, (P.row0 * 2) >> o);
         } else {
           cont = 1;
           pos[0] = R.s; pos[1] = R.m; pos[2] = R.n;
@@ -338,6 +341,17 @@ __global__ __launch_bounds__(256) void k_scatter_kp(const int* __restrict__ stat
   if (i < cap && i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep) out[pos[i]] = kp[i];
 }
 
+// Candidate key of every kept keypoint, in keypoint order (the origin of a
+// keypoint for callers that merge partial results, e.g. row-band shards).
+__global__ __launch_bounds__(256) void k_scatter_key(const int* __restrict__ status,
+                                                     const unsigned* __restrict__ pos,
+                                                     const unsigned* __restrict__ key,
+                                                     const unsigned* __restrict__ n, int cap,
+                                                     unsigned* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < cap && i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep) out[pos[i]] = key[i];
+}
+
 __global__ void k_count_kp(const unsigned* __restrict__ pos, const unsigned* __restrict__ keep,
                            const unsigned* __restrict__ n, unsigned cap, unsigned* __restrict__ out) {
   const unsigned m = min(*n, cap);
@@ -368,6 +382,13 @@ hipError_t launch_scatter_keypoints(const int* status, const unsigned* pos, cons
                                     const unsigned* n, int cap, Keypoint* out, hipStream_t st) {
   if (cap <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_scatter_kp, dim3((cap + 255) / 256), dim3(256), 0, st, status, pos, kp, n, cap, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_keys(const int* status, const unsigned* pos, const unsigned* key, const unsigned* n,
+                               int cap, unsigned* out, hipStream_t st) {
+  if (cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_key, dim3((cap + 255) / 256), dim3(256), 0, st, status, pos, key, n, cap, out);
   return hipGetLastError();
 }
 

@@ -27,6 +27,8 @@ PLANE_GAUSS = 0
 PLANE_DOG = 1
 
 F_SKIP_GAUSS_PLANES = 1
+F_EXPORT_NEXT_SEED = 4
+F_KEYPOINT_ORIGINS = 8
 
 # Exported symbols, exactly those include/sift_hip.h declares.
 ABI_SYMBOLS = (
@@ -38,6 +40,8 @@ ABI_SYMBOLS = (
     "sift_copy_keypoints_device", "sift_detect", "sift_detect_device", "sift_last_counts",
     "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
     "sift_detect_device_async", "sift_detect_wait", "sift_ctx_create_shared",
+    "sift_next_seed", "sift_device_next_seed", "sift_detect_from_seed", "sift_detect_from_seed_device",
+    "sift_keypoint_origins", "sift_set_row_origin",
 )
 
 
@@ -135,6 +139,14 @@ def lib():
         "sift_device_keypoints": (ctypes.c_int, [vp, ctypes.POINTER(vp), szp]),
         "sift_stream": (vp, [vp]),
         "sift_synchronize": (ctypes.c_int, [vp]),
+        "sift_next_seed": (ctypes.c_int, [vp, dp, sz, ip, ip]),
+        "sift_device_next_seed": (ctypes.c_int, [vp, ctypes.POINTER(vp), ip, ip]),
+        "sift_detect_from_seed": (ctypes.c_int, [vp, ctypes.c_int, dp, ctypes.c_int, ctypes.c_int, pp, vp, sz,
+                                                 szp]),
+        "sift_detect_from_seed_device": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, pp, vp,
+                                                        sz, szp]),
+        "sift_keypoint_origins": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int32), sz, szp]),
+        "sift_set_row_origin": (ctypes.c_int, [vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -344,6 +356,42 @@ class Context:
             rc = SIFT_OK
         self._check(rc, "sift_detect_wait")
         return n.value
+
+    # -- row-band shards (include/sift_hip.h, ABI >= 3) ---------------------
+    def next_seed(self):
+        """fp64 base of octave num_octaves from the last build with F_EXPORT_NEXT_SEED."""
+        r, c = ctypes.c_int(), ctypes.c_int()
+        self._check(self._L.sift_next_seed(self._h, None, 0, ctypes.byref(r), ctypes.byref(c)), "sift_next_seed")
+        out = np.empty((r.value, c.value), dtype=np.float64)
+        self._check(self._L.sift_next_seed(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), out.size,
+                                           ctypes.byref(r), ctypes.byref(c)), "sift_next_seed")
+        return out
+
+    def detect_from_seed(self, seed, octave_first, width, height, params, raise_singular=False):
+        """Octaves octave_first.. of a width x height input from that octave's fp64 base."""
+        seed = np.ascontiguousarray(seed, dtype=np.float64)
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect_from_seed(self._h, int(octave_first),
+                                           seed.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(width),
+                                           int(height), ctypes.byref(params), None, 0, ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect_from_seed")
+        self.params, self.width, self.height = params, width, height
+        return self.keypoints()
+
+    def set_row_origin(self, input_row0):
+        """Input row of the first row of the following images (a row-band crop)."""
+        self._check(self._L.sift_set_row_origin(self._h, int(input_row0)), "sift_set_row_origin")
+
+    def keypoint_origins(self):
+        """(n, 4) int32: candidate (octave, scale, y, x) of each keypoint (F_KEYPOINT_ORIGINS)."""
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_keypoint_origins(self._h, None, 0, ctypes.byref(n)), "sift_keypoint_origins")
+        out = np.zeros((max(n.value, 1), 4), dtype=np.int32)
+        self._check(self._L.sift_keypoint_origins(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                  out.size, ctypes.byref(n)), "sift_keypoint_origins")
+        return out[:n.value]
 
     def device_keypoints(self):
         p, n = ctypes.c_void_p(), ctypes.c_size_t()

@@ -1,0 +1,205 @@
+"""Row-band sharding of ONE image over several devices (cfg 5).
+
+The reference runs one image in one Web Worker; there is nothing to mirror
+here beyond its results, which a sharded run reproduces bit for bit.
+
+Octaves depend on each other only through the fp64 base of the next octave
+(background.js:114-118), and every pixel's Gaussian is the same fma chain on
+its clamped neighbourhood (translation invariant in y).  So:
+
+* shard r owns the input rows [lo_r, hi_r) (boundaries at multiples of
+  2^(O-1), whole rows in every octave) and runs the leading octaves 0..K on a
+  crop [c0_r, c1_r) that extends its band by a margin M_K input rows
+  (sift_set_row_origin + sift_detect, num_octaves = K + 1).  Rows at least
+  M_K from an interior crop edge are exactly the whole-image rows: the margin
+  is the sum of the octaves' vertical radii in input rows (a row of octave o
+  reads base rows +-r_o, the base of octave o+1 is octave o's scale S at even
+  rows) plus 8 octave-K rows for the extremum test (+-1) and up to five
+  refinement moves with their 3x3x3 patches;
+* the shard keeps the keypoints whose candidate row it owns and its owned
+  rows of the octave-(K+1) base (SIFT_F_EXPORT_NEXT_SEED);
+* the owned base rows of all shards, in band order, are the whole base of
+  octave K+1; the trailing octaves K+1..O-1 (a few % of the work at 8K: radii
+  double per octave, so a band cannot carry their margins) run from it on one
+  device (sift_detect_from_seed);
+* the keypoints of all shards and the tail, ordered by their candidate
+  (octave, scale, y, x) -- the reference's candidate order -- are the
+  whole-image keypoints.
+
+K is the deepest octave whose margin fits the thinnest band (scaled by
+`max_overhead`), so the redundant halo work stays bounded.
+
+Exchange: the base rows and the keypoint lists are gathered once each
+(all_gather over RCCL/xGMI with torch.distributed, or in-process for a single
+device driving several shards).  No other data crosses devices.
+"""
+import math
+
+import numpy as np
+
+from . import (F_EXPORT_NEXT_SEED, F_KEYPOINT_ORIGINS, KEYPOINT_DTYPE, make_params, octave_dims, schedule)
+
+
+def _js_round(v):
+    f = math.floor(v)
+    return f + 1 if v - f >= 0.5 else f
+
+
+def octave_radii(params):
+    """Blur radius of every (octave, scale) (sift.js:38-44; the octave seed is a copy)."""
+    _, sig = schedule(params)
+    O, NS = sig.shape
+    return [[0 if (o > 0 and s == 0) else int(_js_round(3.0 * sig[o][s])) for s in range(NS)] for o in range(O)]
+
+
+def margin_rows(radii, K):
+    """Input rows a crop needs beyond a band for exact octaves 0..K (see module doc)."""
+    d = 0.0
+    for o in range(K + 1):
+        d += max(radii[o]) * 2.0 ** (o - 1)
+    return int(math.ceil(d + 8 * 2.0 ** (K - 1)))
+
+
+class BandPlan:
+    def __init__(self, width, height, num_octaves, K, bands, crops):
+        self.width, self.height, self.num_octaves = width, height, num_octaves
+        self.K = K                # octaves 0..K on crops; K+1..O-1 from the gathered base
+        self.bands = bands        # owned input rows [lo, hi) per shard
+        self.crops = crops        # crop input rows [c0, c1) per shard
+
+    @property
+    def has_tail(self):
+        return self.K + 1 < self.num_octaves
+
+    def __repr__(self):
+        return "BandPlan(K=%d, bands=%s, crops=%s)" % (self.K, self.bands, self.crops)
+
+
+def plan_bands(width, height, params, n_shards, max_overhead=0.5):
+    """Owned bands, crops and the split octave K for n_shards shards."""
+    O = params.num_octaves
+    align = 2 ** (O - 1)
+    units = -(-height // align)
+    n = max(1, min(int(n_shards), units))
+    cuts = [min(height, (units * r // n) * align) for r in range(n + 1)]
+    cuts[-1] = height
+    bands = [(cuts[r], cuts[r + 1]) for r in range(n)]
+    if n == 1:
+        return BandPlan(width, height, O, O - 1, bands, [(0, height)])
+    band_min = min(hi - lo for lo, hi in bands)
+    radii = octave_radii(params)
+    K = 0
+    for k in range(O - 1, -1, -1):
+        if margin_rows(radii, k) <= max_overhead * band_min:
+            K = k
+            break
+    M = margin_rows(radii, K)
+    step = 2 ** K
+    crops = []
+    for lo, hi in bands:
+        c0 = max(0, lo - M) // step * step
+        c1 = min(height, hi + M)
+        crops.append((c0, c1))
+    return BandPlan(width, height, O, K, bands, crops)
+
+
+def _owned(org, lo, hi, last):
+    """Keypoints whose candidate row (octave rows, column 2 of org) lies in input rows [lo, hi)."""
+    o = org[:, 0]
+    y = org[:, 2]
+    lo_o = np.where(o == 0, 2 * lo, lo >> np.maximum(o - 1, 0))
+    hi_o = np.where(o == 0, 2 * hi, hi >> np.maximum(o - 1, 0))
+    keep = y >= lo_o
+    if not last:
+        keep &= y < hi_o
+    return keep
+
+
+def run_shard(ctx, img, params, plan, r):
+    """Shard r on ctx: (keypoints, origins, owned rows of the octave-(K+1) base or None)."""
+    lo, hi = plan.bands[r]
+    c0, c1 = plan.crops[r]
+    K = plan.K
+    last = r == len(plan.bands) - 1
+    flags = params.flags | F_KEYPOINT_ORIGINS | (F_EXPORT_NEXT_SEED if plan.has_tail else 0)
+    p = make_params(K + 1, params.scales_per_octave, params.min_blur, params.assumed_blur,
+                    params.min_interpixel_distance, flags)
+    ctx.set_row_origin(c0)
+    try:
+        kp = ctx.detect(img[c0:c1], p)
+        org = ctx.keypoint_origins()
+        seed = ctx.next_seed() if plan.has_tail else None
+    finally:
+        ctx.set_row_origin(0)
+    keep = _owned(org, lo, hi, last)
+    part = None
+    if seed is not None:
+        s0 = (lo >> K) - (c0 >> K)
+        s1 = seed.shape[0] if last else (hi >> K) - (c0 >> K)
+        part = np.ascontiguousarray(seed[s0:s1])
+    return kp[keep], org[keep], part
+
+
+def run_tail(ctx, base, params, plan):
+    """Octaves K+1..O-1 of the whole image from the gathered octave-(K+1) base."""
+    p = make_params(params.num_octaves, params.scales_per_octave, params.min_blur, params.assumed_blur,
+                    params.min_interpixel_distance, params.flags | F_KEYPOINT_ORIGINS)
+    h, w = octave_dims(plan.width, plan.height, plan.num_octaves)[plan.K + 1]
+    if base.shape != (h, w):
+        raise ValueError("gathered base %s != octave %d dims %s" % (base.shape, plan.K + 1, (h, w)))
+    kp = ctx.detect_from_seed(base, plan.K + 1, plan.width, plan.height, p)
+    return kp, ctx.keypoint_origins()
+
+
+def merge(parts):
+    """Keypoints of all shards (+ tail) in the reference's candidate order."""
+    kps = [k for k, _ in parts if len(k)]
+    if not kps:
+        return np.zeros(0, dtype=KEYPOINT_DTYPE)
+    kp = np.concatenate(kps)
+    org = np.concatenate([o for k, o in parts if len(k)])
+    order = np.lexsort((org[:, 3], org[:, 2], org[:, 1], org[:, 0]))
+    return kp[order]
+
+
+def detect_sharded_local(ctx, img, params, n_shards, max_overhead=0.5):
+    """All shards on one context in turn (one device): the sharded algorithm
+    without the collectives -- a parity harness and a single-device fallback."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = img.shape
+    plan = plan_bands(W, H, params, n_shards, max_overhead)
+    parts, seeds = [], []
+    for r in range(len(plan.bands)):
+        kp, org, seed = run_shard(ctx, img, params, plan, r)
+        parts.append((kp, org))
+        seeds.append(seed)
+    if plan.has_tail:
+        parts.append(run_tail(ctx, np.concatenate(seeds), params, plan))
+    return merge(parts), plan
+
+
+def detect_sharded(ctx, img, params, group=None, max_overhead=0.5):
+    """One shard per rank of torch.distributed (RCCL on ROCm): every rank
+    passes the same image; all ranks return the whole image's keypoints.
+    Two gathers: the owned base rows (then the tail runs on rank 0) and the
+    keypoint lists."""
+    import torch.distributed as dist
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = img.shape
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    plan = plan_bands(W, H, params, world, max_overhead)
+    mine = []
+    seed = None
+    if rank < len(plan.bands):
+        kp, org, seed = run_shard(ctx, img, params, plan, rank)
+        mine.append((kp, org))
+    if plan.has_tail:
+        seeds = [None] * world
+        dist.all_gather_object(seeds, seed, group=group)
+        if rank == 0:
+            base = np.concatenate([s for s in seeds if s is not None])
+            mine.append(run_tail(ctx, base, params, plan))
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine, group=group)
+    return merge([p for g in gathered for p in g]), plan

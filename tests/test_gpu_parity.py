@@ -246,3 +246,45 @@ def test_async_detect_matches_sync():
             assert a.keypoints().tobytes() == ref and b.keypoints().tobytes() == ref
     finally:
         hip.hipFree(d)
+
+
+# ---------------------------------------------------------------------------
+# Row-band shards of one image (SURVEY.md §8e cfg 5): crops of whole rows for
+# the leading octaves, the gathered fp64 base for the trailing ones.  The
+# merged keypoints must be the whole-image keypoints bit for bit.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("W,H,O,S,n,overhead", [
+    (480, 360, 4, 3, 2, 0.5),
+    (480, 360, 4, 3, 3, 0.5),
+    (640, 600, 5, 3, 4, 0.5),
+    (640, 600, 5, 3, 4, 4.0),    # deeper split octave, more halo
+    (512, 520, 4, 5, 5, 0.05),   # K = 0: octave 0 only on crops
+])
+def test_row_band_shards_match_whole_image(gpu_ctx, W, H, O, S, n, overhead):
+    from sift_amd.shard import detect_sharded_local
+    img = blob_image(W, H, seed=7 + n)
+    p = sift_amd.make_params(O, S)
+    whole = gpu_ctx.detect(img, p).copy()
+    merged, plan = detect_sharded_local(gpu_ctx, img, p, n, max_overhead=overhead)
+    assert len(plan.bands) == n
+    assert merged.shape == whole.shape, (merged.shape, whole.shape, plan)
+    for f in whole.dtype.names:
+        np.testing.assert_array_equal(merged[f], whole[f], err_msg=f)
+
+
+def test_keypoint_origins_and_next_seed(gpu_ctx):
+    """Origins are the candidates of the keypoints; the exported base equals
+    the base a deeper run builds (its octave-O Gaussian scale 0)."""
+    img = blob_image(320, 240, seed=3)
+    p = sift_amd.make_params(3, 3, flags=sift_amd.F_KEYPOINT_ORIGINS | sift_amd.F_EXPORT_NEXT_SEED)
+    kp = gpu_ctx.detect(img, p).copy()
+    org = gpu_ctx.keypoint_origins()
+    assert org.shape == (kp.shape[0], 4)
+    np.testing.assert_array_equal(org[:, 0], kp["octave"])
+    cand = gpu_ctx.candidates()
+    ckeys = set(zip(cand["octave"], cand["scale"], cand["y"], cand["x"]))
+    assert all(tuple(r) in ckeys for r in org.tolist())
+    seed = gpu_ctx.next_seed()
+    p4 = sift_amd.make_params(4, 3)
+    gpu_ctx.build_scale_space(img, p4)
+    np.testing.assert_array_equal(seed.astype(np.float32), gpu_ctx.plane(sift_amd.PLANE_GAUSS, 3, 0))
