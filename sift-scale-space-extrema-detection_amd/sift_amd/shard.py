@@ -34,6 +34,7 @@ Exchange: the base rows and the keypoint lists are gathered once each
 device driving several shards).  No other data crosses devices.
 """
 import math
+import time
 
 import numpy as np
 
@@ -115,8 +116,17 @@ def _owned(org, lo, hi, last):
     return keep
 
 
-def run_shard(ctx, img, params, plan, r):
-    """Shard r on ctx: (keypoints, origins, owned rows of the octave-(K+1) base or None)."""
+def _tick(timer, key, t0):
+    if timer is not None:
+        t = time.perf_counter()
+        timer[key] = timer.get(key, 0.0) + t - t0
+        return t
+    return t0
+
+
+def run_shard(ctx, img, params, plan, r, timer=None):
+    """Shard r on ctx: (keypoints, origins, owned rows of the octave-(K+1) base or None).
+    timer: optional dict accumulating wall seconds per step."""
     lo, hi = plan.bands[r]
     c0, c1 = plan.crops[r]
     K = plan.K
@@ -125,10 +135,14 @@ def run_shard(ctx, img, params, plan, r):
     p = make_params(K + 1, params.scales_per_octave, params.min_blur, params.assumed_blur,
                     params.min_interpixel_distance, flags)
     ctx.set_row_origin(c0)
+    t0 = time.perf_counter()
     try:
         kp = ctx.detect(img[c0:c1], p)
+        t0 = _tick(timer, "detect", t0)
         org = ctx.keypoint_origins()
+        t0 = _tick(timer, "origins", t0)
         seed = ctx.next_seed() if plan.has_tail else None
+        t0 = _tick(timer, "seed", t0)
     finally:
         ctx.set_row_origin(0)
     keep = _owned(org, lo, hi, last)
@@ -137,7 +151,9 @@ def run_shard(ctx, img, params, plan, r):
         s0 = (lo >> K) - (c0 >> K)
         s1 = seed.shape[0] if last else (hi >> K) - (c0 >> K)
         part = np.ascontiguousarray(seed[s0:s1])
-    return kp[keep], org[keep], part
+    out = kp[keep], org[keep], part
+    _tick(timer, "filter", t0)
+    return out
 
 
 def run_tail(ctx, base, params, plan):

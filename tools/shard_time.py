@@ -31,11 +31,12 @@ for _ in range(reps):
     t_whole.append(time.perf_counter() - t0)
 plan = shard.plan_bands(W, H, p, n)
 t_parts, seeds, parts = [], [], []
+steps = {}
 for rep in range(reps + 1):
     tp, seeds, parts = [], [], []
     for r in range(len(plan.bands)):
         t0 = time.perf_counter()
-        kp, org, seed = shard.run_shard(ctx, img, p, plan, r)
+        kp, org, seed = shard.run_shard(ctx, img, p, plan, r, timer=steps if rep else None)
         tp.append(time.perf_counter() - t0)
         parts.append((kp, org))
         seeds.append(seed)
@@ -55,4 +56,5 @@ print(json.dumps({"config": "8K 7680x4320 O6 S5, host image in/keypoints out (in
                   "tail_ms": round(1e3 * float(tp[-1]), 3),
                   "sum_ms": round(1e3 * float(tp.sum()), 3),
                   "critical_path_ms": round(1e3 * float(tp[:-1].max() + tp[-1]), 3),
+                  "shard_steps_ms_per_rep": {k: round(1e3 * v / reps, 3) for k, v in steps.items()},
                   "keypoints": int(whole.shape[0]), "identical": bool(same)}))
