@@ -99,12 +99,14 @@ def main():
     ap.add_argument("--scales", type=int, default=5)
     ap.add_argument("--skip-gauss-planes", action="store_true",
                     help="keypoints-only mode: do not materialise the Gaussian planes")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="detections in flight per GPU: contexts on ONE stream, so image k+1 is queued "
-                         "behind image k (no kernel overlap) while the host settles image k")
-    ap.add_argument("--independent-streams", action="store_true",
-                    help="in-flight detections on their own streams: kernels of consecutive images overlap "
-                         "(higher Mpix/s; per-kernel durations, hence roofline.achieved, include the overlap)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="detections in flight per GPU (one context each; the host settles image k while "
+                         "image k+1 runs)")
+    ap.add_argument("--overlap", default="octave0", choices=["none", "octave0", "gaussian", "refinement", "full"],
+                    help="how consecutive images overlap on the GPU: none = contexts share one stream; "
+                         "octave0 / gaussian / refinement = own streams, image k+1 starts once image k has "
+                         "passed that point (sift_order_after: software pipelining); full = own streams, "
+                         "no ordering.  Per-kernel durations (roofline.achieved) include any overlap")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
     args = ap.parse_args()
@@ -137,7 +139,10 @@ def main():
     torch.cuda.synchronize(dev)
     nin = max(1, args.inflight)
     ctxs = [sift_amd.Context(dev)]
-    ctxs += [sift_amd.Context(dev, share=None if args.independent_streams else ctxs[0]) for _ in range(nin - 1)]
+    own = args.overlap != "none"
+    after = {"octave0": sift_amd.AFTER_OCTAVE0, "gaussian": sift_amd.AFTER_GAUSSIAN,
+             "refinement": sift_amd.AFTER_REFINEMENT}.get(args.overlap)
+    ctxs += [sift_amd.Context(dev, share=None if own else ctxs[0]) for _ in range(nin - 1)]
     ctx = ctxs[0]
 
     gather = None
@@ -148,6 +153,8 @@ def main():
     stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0, "gauss_oct0_ms": 0.0}
 
     def launch(i):
+        if after is not None and i > 0 and nin > 1:
+            ctxs[i % nin].order_after(ctxs[(i - 1) % nin], after)
         ctxs[i % nin].detect_device_async(d_img.data_ptr(), W, H, params)
 
     def finish(i, acc):
@@ -221,7 +228,8 @@ def main():
                             (W, H, O, S, ", Gaussian planes not materialised" if args.skip_gauss_planes else ""),
                 "width": W, "height": H, "octaves": O, "scales_per_octave": S,
                 "images_per_gpu": 1, "global_batch": world, "inflight_per_gpu": nin,
-                "streams_per_gpu": nin if args.independent_streams else 1,
+                "streams_per_gpu": nin if own else 1,
+                "overlap": args.overlap,
                 "parallelism": "dp%d (one image per GPU, RCCL keypoint all-gather)" % world if world > 1 else "single GPU",
                 "planes": "fp32 out, fp64 accumulation/seeds",
             },

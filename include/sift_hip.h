@@ -207,6 +207,19 @@ int sift_detect_device_async(struct sift_ctx *ctx, const float *d_img, int width
                              size_t stride_px, const sift_params *p);
 int sift_detect_wait(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out);
 
+/* Software pipelining of consecutive images on contexts with their own
+ * streams (ABI version >= 3): the next work enqueued on ctx waits until
+ * prev's last enqueued detection has passed `after`:
+ *   SIFT_AFTER_OCTAVE0     its octave-0 Gaussian+DoG (HBM-write bound) -- the
+ *                          next image's octave 0 then overlaps prev's small
+ *                          octaves, extrema scan and refinement;
+ *   SIFT_AFTER_GAUSSIAN    its whole Gaussian+DoG pass;
+ *   SIFT_AFTER_REFINEMENT  its fast refinement (only the latency-bound tail
+ *                          overlaps).
+ * No-op for contexts sharing one stream (already in order). */
+enum { SIFT_AFTER_OCTAVE0 = 0, SIFT_AFTER_GAUSSIAN = 1, SIFT_AFTER_REFINEMENT = 2 };
+int sift_order_after(struct sift_ctx *ctx, const struct sift_ctx *prev, int after);
+
 int sift_last_timings(struct sift_ctx *ctx, sift_timings *t);
 
 /* Device-to-device copy of the last keypoints into caller device memory

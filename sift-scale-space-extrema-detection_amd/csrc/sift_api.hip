@@ -96,6 +96,7 @@ struct sift_ctx {
   DBuf counters, temp;
   unsigned* h_counters = nullptr;              // pinned mirror of counters
   hipEvent_t ev[8]{};
+  hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
   sift_timings tm{};
 };
 
@@ -190,6 +191,7 @@ static int ctx_create(int device, sift_ctx* share, sift_ctx** out) {
     return SIFT_E_HIP;
   }
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  (void)hipEventCreateWithFlags(&ctx->ev_heavy, hipEventDisableTiming);
   // Measured on MI355X at 4K: overlapping the memory-bound scans with the
   // small octaves' Gaussians slows both (shared L2/fabric), so the overlap
   // is opt-in (SIFT_SIDE_STREAM=1).
@@ -227,6 +229,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->ev_heavy) (void)hipEventDestroy(ctx->ev_heavy);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
   for (auto& e : ctx->ev_oct)
     if (e) (void)hipEventDestroy(e);
@@ -783,6 +786,7 @@ static int refine_enqueue(sift_ctx* ctx) {
     R.uncertain = ctx->uncertain.as<unsigned>();
     R.counters = cnt;
     HIPCHK(launch_refine_fast(P, R, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_heavy, ctx->stream));  // the rest is latency-bound tail work
     // Uncertain decisions exist only with fp32-rounded native planes.
     if (ctx->dog_source == kNative) HIPCHK(launch_refine_exact(P, R, ctx->stream));
     HIPCHK(launch_status_to_keep(R.status, ctx->keep.as<unsigned>(), R.n, cap, ctx->stream));
@@ -1130,6 +1134,19 @@ int sift_detect_from_seed(sift_ctx* ctx, int octave_first, const double* seed, i
 int sift_detect_from_seed_device(sift_ctx* ctx, int octave_first, const double* d_seed, int width, int height,
                                  const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
   return detect_from_seed(ctx, octave_first, nullptr, d_seed, width, height, p, out, cap, n_out);
+}
+
+int sift_order_after(sift_ctx* ctx, const sift_ctx* prev, int after) {
+  if (!ctx || !prev) return SIFT_E_ARG;
+  if (after < SIFT_AFTER_OCTAVE0 || after > SIFT_AFTER_REFINEMENT) return SIFT_E_ARG;
+  if (ctx == prev || ctx->stream == prev->stream) return SIFT_OK;  // already ordered
+  HIPCHK(hipSetDevice(ctx->device));
+  // ev[7]: octave 0's Gaussian+DoG done; ev[2]: all octaves; ev_heavy: the
+  // fast refinement (the rest is the latency-bound tail).
+  const hipEvent_t e = after == SIFT_AFTER_OCTAVE0 ? prev->ev[7] : after == SIFT_AFTER_GAUSSIAN ? prev->ev[2]
+                                                                                                 : prev->ev_heavy;
+  HIPCHK(hipStreamWaitEvent(ctx->stream, e, 0));
+  return SIFT_OK;
 }
 
 int sift_set_row_origin(sift_ctx* ctx, int input_row0) {

@@ -30,6 +30,10 @@ F_SKIP_GAUSS_PLANES = 1
 F_EXPORT_NEXT_SEED = 4
 F_KEYPOINT_ORIGINS = 8
 
+AFTER_OCTAVE0 = 0
+AFTER_GAUSSIAN = 1
+AFTER_REFINEMENT = 2
+
 # Exported symbols, exactly those include/sift_hip.h declares.
 ABI_SYMBOLS = (
     "sift_abi_version", "sift_params_default", "sift_ctx_create", "sift_ctx_destroy",
@@ -41,7 +45,7 @@ ABI_SYMBOLS = (
     "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
     "sift_detect_device_async", "sift_detect_wait", "sift_ctx_create_shared",
     "sift_next_seed", "sift_device_next_seed", "sift_detect_from_seed", "sift_detect_from_seed_device",
-    "sift_keypoint_origins", "sift_set_row_origin",
+    "sift_keypoint_origins", "sift_set_row_origin", "sift_order_after",
 )
 
 
@@ -147,6 +151,7 @@ def lib():
                                                         sz, szp]),
         "sift_keypoint_origins": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int32), sz, szp]),
         "sift_set_row_origin": (ctypes.c_int, [vp, ctypes.c_int]),
+        "sift_order_after": (ctypes.c_int, [vp, vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -347,6 +352,12 @@ class Context:
                                                      int(stride or width), ctypes.byref(params)),
                     "sift_detect_device_async")
         self.params, self.width, self.height = params, width, height
+
+    def order_after(self, prev, after=0):
+        """Next work on this context waits until prev's last detection has
+        passed `after` (AFTER_OCTAVE0 / AFTER_GAUSSIAN / AFTER_REFINEMENT,
+        sift_order_after): software pipelining of consecutive images."""
+        self._check(self._L.sift_order_after(self._h, prev._h, int(after)), "sift_order_after")
 
     def detect_wait(self, raise_singular=False):
         """Complete the detection in flight; returns the keypoint count."""
