@@ -195,6 +195,17 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    # After the timed region: the same detection alone (one image in flight,
+    # nothing overlapping), so the kernel's isolated duration is on record
+    # beside its pipelined one.
+    iso = {"gauss_dog_ms": 0.0, "gauss_oct0_ms": 0.0}
+    n_iso = 5
+    for _ in range(n_iso):
+        ctx.detect_device_async(d_img.data_ptr(), W, H, params)
+        ctx.detect_wait()
+        t = ctx.timings()
+        for k in iso:
+            iso[k] += t[k] / n_iso
     K = args.steps
     ms_per_step = elapsed / K * 1e3
     value = world * W * H / (elapsed / K) / 1e6
@@ -250,6 +261,18 @@ def main():
                 "alg_bytes_formula": ("4WH + 4P_0(S+2)" if args.skip_gauss_planes
                                       else "4WH + 4P_0(S+3) + 4P_0(S+2)"),
                 "launch_ms": round(oct0_ms, 5),
+                "measured": ("HIP events around the launch on its stream, averaged over the timed region%s" %
+                             ("" if args.overlap == "none" or nin == 1 else
+                              " (pipelined: includes waiting for CUs held by the previous image's kernels)")),
+                "isolated": {
+                    "what": "same launch, one image in flight, nothing overlapping (%d images after the timed "
+                            "region)" % n_iso,
+                    "launch_ms": round(iso["gauss_oct0_ms"], 5),
+                    "achieved": round(B0 / (iso["gauss_oct0_ms"] * 1e-3) / 1e9, 1),
+                    "frac": round(B0 / (iso["gauss_oct0_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "stage_ms": round(iso["gauss_dog_ms"], 5),
+                    "stage_frac": round(B / (iso["gauss_dog_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                },
                 "stage": {
                     "what": "whole Gaussian+DoG pass, %d launches (one per octave)" % O,
                     "alg_bytes": B,

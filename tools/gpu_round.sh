@@ -20,6 +20,8 @@ cat $O/bench_$TAG.json
 cd /tmp
 echo "[$(date +%T)] kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_prof_$TAG.json 2> $O/prof_$TAG.err || { echo "trace failed"; tail -5 $O/prof_$TAG.err; exit 1; }
+echo "[$(date +%T)] kernel trace, --overlap none (isolated kernels)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_iso -o run -- python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --overlap none --inflight 2 > $O/bench_prof_${TAG}_iso.json 2> $O/prof_${TAG}_iso.err || { echo "trace failed"; tail -5 $O/prof_${TAG}_iso.err; exit 1; }
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "[$(date +%T)] pmc $C"
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${TAG}_$C -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> $O/pmc_${TAG}_$C.err || { echo "pmc $C failed"; tail -5 $O/pmc_${TAG}_$C.err; exit 1; }
