@@ -215,9 +215,25 @@ __device__ inline void make_keypoint(Keypoint& k, int o, const StepOut& R, int S
   k.interp_value = R.omega;
 }
 
+#ifndef SIFT_REFINE_XCD
+#define SIFT_REFINE_XCD 1
+#endif
+// Candidates are in raster order per (octave, scale), so neighbouring slots
+// gather overlapping DoG lines.  Blocks are dispatched round-robin over the
+// 8 XCDs (separate L2s): block b runs the logical block of a contiguous range
+// per XCD, so those shared lines hit in one L2 instead of being fetched by
+// every XCD.  A bijection over the live blocks (the count is on the device).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  constexpr int kXcd = 8;
+  const int q = nb / kXcd, r = nb % kXcd, x = b % kXcd;
+  return x * q + min(x, r) + b / kXcd;
+}
+
 __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const RefineLaunch L) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = (int)min(*L.n, (unsigned)L.cap);
+  const int nb = (n + 255) / 256;
+  if ((int)blockIdx.x >= nb) return;  // whole block past the live slots
+  const int i = (SIFT_REFINE_XCD ? xcd_block(blockIdx.x, nb) : (int)blockIdx.x) * 256 + threadIdx.x;
   bool unc = false;
   if (i < n && L.keep && !L.keep[i]) {
     L.status[i] = kRefDiscard;
