@@ -4,7 +4,7 @@ HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 PKG     := sift-scale-space-extrema-detection_amd
 CSRC    := $(PKG)/csrc
-HIPSRC  := $(CSRC)/sift_gauss.hip $(CSRC)/sift_extrema.hip $(CSRC)/sift_refine.hip $(CSRC)/sift_api.hip
+HIPSRC  := $(CSRC)/sift_gauss.hip $(CSRC)/sift_extrema.hip $(CSRC)/sift_refine.hip $(CSRC)/sift_image.hip $(CSRC)/sift_api.hip
 HDRS    := $(wildcard $(CSRC)/*.h) include/sift_hip.h
 HIPFLAGS ?= --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result
 LIB     := $(PKG)/libsift_hip.so

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 3
+#define SIFT_ABI_VERSION 4
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -269,6 +269,46 @@ int sift_detect_from_seed_device(struct sift_ctx *ctx, int octave_first, const d
  * detection/refinement run with SIFT_F_KEYPOINT_ORIGINS: 4 int32 per
  * keypoint, keypoint order (the reference's candidate order). */
 int sift_keypoint_origins(struct sift_ctx *ctx, int32_t *out, size_t cap, size_t *n_out);
+
+/* ---- Image products either side of the path (ABI version >= 4) ---------- */
+
+/* ImageUtils_convertImageDataToMatrix2D({convertToGrayscale: true,
+ * usePerceptualGrayscale: true}) (image-utils.js:27-152, called by
+ * main.js:98-103) on device: gray = ((R*0.299) + (G*0.587) + (B*0.114)) / 255,
+ * alpha = A / 255, evaluated in fp64 in that order and rounded once to fp32
+ * (bit-identical to Float32Array.from(<the reference's gray Matrix2D>)).
+ * `rgba` is ImageData.data (Uint8 R,G,B,A per pixel, row stride in bytes, a
+ * multiple of 4); `gray` (required) and `alpha` (NULL = discardAlphaChannel)
+ * are dense width*height fp32.  Host buffers here, device buffers in the
+ * _device form (ordered on ctx's stream, completed before return). */
+int sift_rgba_to_gray(struct sift_ctx *ctx, const uint8_t *rgba, int width, int height, size_t stride_bytes,
+                      float *gray, float *alpha);
+int sift_rgba_to_gray_device(struct sift_ctx *ctx, const uint8_t *d_rgba, int width, int height,
+                             size_t stride_bytes, float *d_gray, float *d_alpha);
+
+/* sift_build_scale_space / sift_detect from an RGBA ImageData (host): the
+ * RGBA bytes are uploaded and converted on device (no host gray pass). */
+int sift_build_scale_space_rgba(struct sift_ctx *ctx, const uint8_t *rgba, int width, int height,
+                                size_t stride_bytes, const sift_params *p, const double *offset_sigmas);
+int sift_detect_rgba(struct sift_ctx *ctx, const uint8_t *rgba, int width, int height, size_t stride_bytes,
+                     const sift_params *p, sift_keypoint *out, size_t cap, size_t *n_out);
+
+/* Preview ImageData of one plane of the context's pyramid, as the reference
+ * posts them to its UI: ImageUtils_convertMatrix2DToImageData with a gray
+ * channel (image-utils.js:171-217): p = Math.round(g * 255) stored as
+ * (p, p, p, 255) with Uint8ClampedArray clamping, where g is
+ *   SIFT_DISPLAY_PLAIN    the plane value (Gaussian images, background.js:139, :218)
+ *   SIFT_DISPLAY_SIGMOID  1/(1+exp(coefficient*(-1*v))) (Matrix2D_sigmoidNormalize,
+ *                         matrix2d.js:151; DoG chunks use 5, background.js:303)
+ *   SIFT_DISPLAY_SAMPLED  (v-min)/(max-min) over the plane (Matrix2D_sampledNormalize,
+ *                         matrix2d.js:169; DoG images, background.js:336, :387)
+ * computed in fp64 from the fp32 plane.  `rgba` holds rows*cols*4 bytes
+ * (cap_bytes); host memory, or device memory in the _device form. */
+enum { SIFT_DISPLAY_PLAIN = 0, SIFT_DISPLAY_SIGMOID = 1, SIFT_DISPLAY_SAMPLED = 2 };
+int sift_plane_image(struct sift_ctx *ctx, int kind, int octave, int scale, int mode, double coefficient,
+                     uint8_t *rgba, size_t cap_bytes);
+int sift_plane_image_device(struct sift_ctx *ctx, int kind, int octave, int scale, int mode,
+                            double coefficient, uint8_t *d_rgba, size_t cap_bytes);
 
 /* Wait for all work queued on ctx's stream. */
 int sift_synchronize(struct sift_ctx *ctx);

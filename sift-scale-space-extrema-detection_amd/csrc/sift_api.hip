@@ -94,6 +94,7 @@ struct sift_ctx {
   DBuf status, kp_tmp, kp, uncertain;          // refinement
   DBuf xseed, kp_key;                          // next-octave base, keypoint origins
   DBuf counters, temp;
+  DBuf rgba, alpha, display, mm_parts;         // image products (sift_image.hip)
   unsigned* h_counters = nullptr;              // pinned mirror of counters
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
@@ -225,7 +226,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->xseed, &ctx->kp_key, &ctx->counters,
-                  &ctx->temp};
+                  &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1147,6 +1148,113 @@ int sift_order_after(sift_ctx* ctx, const sift_ctx* prev, int after) {
                                                                                                  : prev->ev_heavy;
   HIPCHK(hipStreamWaitEvent(ctx->stream, e, 0));
   return SIFT_OK;
+}
+
+// ---- Image products either side of the path (sift_image.hip) -------------
+
+static int check_rgba(sift_ctx* ctx, const void* rgba, int W, int H, size_t stride_bytes) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!rgba || W <= 0 || H <= 0) return set_err(ctx, SIFT_E_ARG, "null or empty RGBA image");
+  if (stride_bytes < (size_t)W * 4 || stride_bytes % 4) return set_err(ctx, SIFT_E_ARG, "bad RGBA row stride");
+  return SIFT_OK;
+}
+
+// Upload the RGBA rows (dense) and convert them into ctx->img on ctx's stream.
+static int rgba_to_ctx_img(sift_ctx* ctx, const uint8_t* rgba, int W, int H, size_t stride_bytes,
+                           bool alpha = false) {
+  int rc = check_rgba(ctx, rgba, W, H, stride_bytes);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(ctx->rgba.ensure((size_t)W * H * 4));
+  HIPCHK(ctx->img.ensure((size_t)W * H * sizeof(float)));
+  HIPCHK(hipMemcpy2DAsync(ctx->rgba.p, (size_t)W * 4, rgba, stride_bytes, (size_t)W * 4, H, hipMemcpyHostToDevice,
+                          ctx->stream));
+  if (alpha) HIPCHK(ctx->alpha.ensure((size_t)W * H * sizeof(float)));
+  HIPCHK(launch_rgba_to_gray(ctx->rgba.as<unsigned char>(), (size_t)W * 4, W, H, ctx->img.as<float>(),
+                             alpha ? ctx->alpha.as<float>() : nullptr, ctx->stream));
+  return SIFT_OK;
+}
+
+int sift_rgba_to_gray_device(sift_ctx* ctx, const uint8_t* d_rgba, int width, int height, size_t stride_bytes,
+                             float* d_gray, float* d_alpha) {
+  int rc = check_rgba(ctx, d_rgba, width, height, stride_bytes);
+  if (rc) return rc;
+  if (!d_gray) return set_err(ctx, SIFT_E_ARG, "null gray destination");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(launch_rgba_to_gray(d_rgba, stride_bytes, width, height, d_gray, d_alpha, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+int sift_rgba_to_gray(sift_ctx* ctx, const uint8_t* rgba, int width, int height, size_t stride_bytes, float* gray,
+                      float* alpha) {
+  if (ctx && !gray) return set_err(ctx, SIFT_E_ARG, "null gray destination");
+  int rc = rgba_to_ctx_img(ctx, rgba, width, height, stride_bytes, alpha != nullptr);
+  if (rc) return rc;
+  const size_t n = (size_t)width * height;
+  if (alpha) HIPCHK(hipMemcpyAsync(alpha, ctx->alpha.p, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(gray, ctx->img.p, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+int sift_build_scale_space_rgba(sift_ctx* ctx, const uint8_t* rgba, int width, int height, size_t stride_bytes,
+                                const sift_params* p, const double* sig) {
+  int rc = rgba_to_ctx_img(ctx, rgba, width, height, stride_bytes);
+  if (rc) return rc;
+  return sift_build_scale_space_device(ctx, ctx->img.as<float>(), width, height, (size_t)width, p, sig);
+}
+
+int sift_detect_rgba(sift_ctx* ctx, const uint8_t* rgba, int width, int height, size_t stride_bytes,
+                     const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
+  int rc = rgba_to_ctx_img(ctx, rgba, width, height, stride_bytes);
+  if (rc) return rc;
+  return detect_common(ctx, nullptr, ctx->img.as<float>(), width, height, (size_t)width, p, out, cap, n_out);
+}
+
+static int plane_image_common(sift_ctx* ctx, int kind, int o, int s, int mode, double coef, uint8_t* dst,
+                              size_t cap_bytes, bool host) {
+  if (!ctx || !dst) return SIFT_E_ARG;
+  if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no pyramid");
+  if (mode < SIFT_DISPLAY_PLAIN || mode > SIFT_DISPLAY_SAMPLED) return set_err(ctx, SIFT_E_ARG, "bad display mode");
+  const Pyramid& P = ctx->P;
+  if (o < 0 || o >= P.O) return set_err(ctx, SIFT_E_ARG, "octave out of range");
+  if (o < ctx->o_first) return set_err(ctx, SIFT_E_STATE, "octave not built (sift_detect_from_seed)");
+  const Octave& oc = P.oct[o];
+  const size_t plane = (size_t)oc.h * oc.w;
+  if (cap_bytes < plane * 4) return set_err(ctx, SIFT_E_CAPACITY, "destination too small (4 bytes per pixel)");
+  const float* src = nullptr;
+  if (kind == SIFT_PLANE_GAUSS) {
+    if (!ctx->have_gauss) return set_err(ctx, SIFT_E_STATE, "Gaussian planes not materialised");
+    if (s < 0 || s >= P.NS) return set_err(ctx, SIFT_E_ARG, "scale out of range");
+    src = ctx->gauss.as<float>() + oc.gauss_off + (size_t)s * plane;
+  } else if (kind == SIFT_PLANE_DOG) {
+    if (s < 0 || s >= P.ND) return set_err(ctx, SIFT_E_ARG, "scale out of range");
+    src = ctx->dog.as<float>() + oc.dog_off + (size_t)s * plane;
+  } else {
+    return set_err(ctx, SIFT_E_ARG, "bad plane kind");
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(ctx->mm_parts.ensure((size_t)plane_image_parts((long long)plane) * sizeof(float2)));
+  unsigned* out = reinterpret_cast<unsigned*>(dst);
+  if (host) {
+    HIPCHK(ctx->display.ensure(plane * 4));
+    out = ctx->display.as<unsigned>();
+  }
+  HIPCHK(launch_plane_image(src, (long long)plane, mode, coef, ctx->mm_parts.as<float2>(), out, ctx->stream));
+  if (host) HIPCHK(hipMemcpyAsync(dst, out, plane * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+int sift_plane_image(sift_ctx* ctx, int kind, int octave, int scale, int mode, double coefficient, uint8_t* rgba,
+                     size_t cap_bytes) {
+  return plane_image_common(ctx, kind, octave, scale, mode, coefficient, rgba, cap_bytes, true);
+}
+
+int sift_plane_image_device(sift_ctx* ctx, int kind, int octave, int scale, int mode, double coefficient,
+                            uint8_t* d_rgba, size_t cap_bytes) {
+  return plane_image_common(ctx, kind, octave, scale, mode, coefficient, d_rgba, cap_bytes, false);
 }
 
 int sift_set_row_origin(sift_ctx* ctx, int input_row0) {

@@ -124,4 +124,13 @@ hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, con
 
 size_t exact_lds_bytes(const Pyramid& P);
 
+// Image products either side of the path (sift_image.hip).
+// gray/alpha rows are dense (w floats); alpha may be nullptr.
+hipError_t launch_rgba_to_gray(const unsigned char* rgba, size_t stride_bytes, int w, int h, float* gray,
+                               float* alpha, hipStream_t st);
+// float2 partials needed by the sampled mode for an n-pixel plane.
+int plane_image_parts(long long n);
+hipError_t launch_plane_image(const float* plane, long long n, int mode, double coefficient, float2* parts,
+                              unsigned* out, hipStream_t st);
+
 }  // namespace sift

@@ -11,7 +11,9 @@
 // one-call detect()/detectAsync().
 //
 // Images are ImageData-shaped gray Float32: {width, height, data: Float32Array}.
-// A Matrix2D (nested arrays, matrix2d.js) is accepted and rounded to fp32.
+// A Matrix2D (nested arrays, matrix2d.js) is accepted and rounded to fp32; an
+// RGBA ImageData (Uint8ClampedArray data) is converted to gray on the device
+// with the reference's perceptual weights (image-utils.js:27-152).
 // Planes come back ImageData-shaped, or as Matrix2D with {matrix2d: true}
 // (what main.js-style callers index as image[y][x]).
 //
@@ -88,7 +90,13 @@ function isMatrix2D(m) {
   return Array.isArray(m) && m.length > 0 && (Array.isArray(m[0]) || ArrayBuffer.isView(m[0]));
 }
 
+function isRgba(img) {
+  return !!img && (img.data instanceof Uint8ClampedArray || img.data instanceof Uint8Array) && img.width > 0 &&
+    img.height > 0 && img.data.length === img.width * img.height * 4;
+}
+
 function toGray(img) {
+  if (isRgba(img)) return { width: img.width, height: img.height, data: img.data, rgba: true };
   if (img && ArrayBuffer.isView(img.data) && img.width > 0 && img.height > 0) {
     const n = img.width * img.height;
     if (img.data.length < n) throw new TypeError('image.data is shorter than width*height');
@@ -189,7 +197,8 @@ export function computeGaussianScaleSpace(args, ...rest) {
   const st = deviceState(device);
   const { blur, sigma } = scaleSchedule(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur);
   const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur);
-  native.buildScaleSpace(st.ctx, img.data, img.width, img.height, params, sigma);
+  if (img.rgba) native.buildScaleSpaceRgba(st.ctx, img.data, img.width, img.height, params, sigma);
+  else native.buildScaleSpace(st.ctx, img.data, img.width, img.height, params, sigma);
   const gen = bump(st, 'built', img.width, img.height, params);
   const NS = scales_per_octave + 3;
   const scaleSpace = [];
@@ -201,7 +210,7 @@ export function computeGaussianScaleSpace(args, ...rest) {
     }
     scaleSpace.push(oct);
   }
-  return attach(scaleSpace, st, gen, { blur, matrix2d, params });
+  return attach(scaleSpace, st, gen, { blur, matrix2d, params, kind: PLANE_GAUSS });
 }
 export const buildScaleSpace = computeGaussianScaleSpace;
 
@@ -238,7 +247,7 @@ export function computeDifferenceOfGaussians(scale_space, chunk_size = 32, { dev
     }
     dog.push(oct);
   }
-  return attach(dog, st, gen, {});
+  return attach(dog, st, gen, { kind: PLANE_DOG });
 }
 
 function ensureDog(differenceOfGaussians, scalesPerOctave, device) {
@@ -254,7 +263,7 @@ function ensureDog(differenceOfGaussians, scalesPerOctave, device) {
   const params = nativeParams(O, S, 0.8, 0.5);
   native.loadDog(st.ctx, flatten(differenceOfGaussians), W, H, params);
   const gen = bump(st, 'foreign-dog', W, H, params);
-  attach(differenceOfGaussians, st, gen, {});
+  attach(differenceOfGaussians, st, gen, { kind: PLANE_DOG });
   return st;
 }
 
@@ -352,7 +361,8 @@ export function detect(input_image, { number_of_octaves = 5, scales_per_octave =
   const img = toGray(input_image);
   const st = deviceState(device);
   const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
-  const r = native.detect(st.ctx, img.data, img.width, img.height, params);
+  const r = img.rgba ? native.detectRgba(st.ctx, img.data, img.width, img.height, params)
+    : native.detect(st.ctx, img.data, img.width, img.height, params);
   bump(st, 'detected', img.width, img.height, params);
   return keypointsFromNative(r);
 }
@@ -360,8 +370,9 @@ export function detect(input_image, { number_of_octaves = 5, scales_per_octave =
 export async function detectAsync(input_image, opts = {}) {
   const { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8, assumed_blur = 0.5,
     min_interpixel_distance = 0.5, device = 0 } = opts;
-  const img = toGray(input_image);
+  let img = toGray(input_image);
   const st = deviceState(device);
+  if (img.rgba) img = { width: img.width, height: img.height, data: native.rgbaToGray(st.ctx, img.data, img.width, img.height, false).gray };
   const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
   bump(st, 'detecting', img.width, img.height, params);
   const r = await native.detectAsync(st.ctx, img.data, img.width, img.height, params);
@@ -373,30 +384,99 @@ export function lastCounts(device = 0) {
 }
 
 // ---------------------------------------------------------------------------
+// Image products either side of the path (SURVEY.md §8f rows 2-3), on device.
+// ---------------------------------------------------------------------------
+
+// ImageUtils_convertImageDataToMatrix2D (image-utils.js:27-152), gray forms:
+// gray = ((R*0.299) + (G*0.587) + (B*0.114)) / 255 (both grayscale flavours
+// use the perceptual weights in the reference) and alpha = A / 255, returned
+// as the reference returns them (gray, or [gray, alpha]) -- Matrix2D, or
+// ImageData-shaped Float32 with {matrix2d: false}.  Values are the fp32
+// rounding of the reference's fp64 ones (the path's Float32 image contract).
+export function convertImageDataToMatrix2D({ imageData, convertToGrayscale = false, usePerceptualGrayscale = false,
+  discardAlphaChannel = false, device = 0, matrix2d = true } = {}) {
+  void usePerceptualGrayscale;  // image-utils.js:106-111: both branches use the perceptual weights
+  if (convertToGrayscale !== true) {
+    throw new RangeError('only the grayscale conversion feeds the SIFT path; split RGB channels on the host');
+  }
+  if (!isRgba(imageData)) throw new TypeError('expected an RGBA ImageData {width, height, data: Uint8ClampedArray}');
+  const { width, height } = imageData;
+  const r = native.rgbaToGray(deviceState(device).ctx, imageData.data, width, height, !discardAlphaChannel);
+  const gray = planeImage(r.gray, width, height, matrix2d);
+  return discardAlphaChannel ? gray : [gray, planeImage(r.alpha, width, height, matrix2d)];
+}
+
+const DISPLAY_MODES = { plain: 0, sigmoid: 1, sampled: 2 };
+
+// Preview ImageData of plane (octave, scale) of a live stage result (the
+// scale space or the DoG pyramid), as ImageUtils_convertMatrix2DToImageData
+// (image-utils.js:171-217) makes them from the plain plane (Gaussian
+// images, background.js:139/:218), Matrix2D_sigmoidNormalize(.., coefficient)
+// (DoG chunks, background.js:303) or Matrix2D_sampledNormalize (DoG images,
+// background.js:336/:387).  Chunk previews are crops of the whole-plane ones.
+export function planeImageData(pyramid, octave, scale, { mode = 'plain', coefficient = 5 } = {}) {
+  const h = liveHandle(pyramid);
+  if (!h || h.kind === undefined) throw new TypeError('expected a live scale-space or difference-of-Gaussians result');
+  const m = DISPLAY_MODES[mode];
+  if (m === undefined) throw new RangeError('mode must be plain, sigmoid or sampled');
+  const [rows, cols] = native.getDims(h.st.ctx, octave);
+  return { width: cols, height: rows, data: native.planeImage(h.st.ctx, h.kind, octave, scale, m, coefficient) };
+}
+
+// ---------------------------------------------------------------------------
 // background.js-compatible dispatcher (background.js:14-50): returns an
 // onmessage(e) that answers each request with the reference's RECEIVED_*
 // message.  Pyramids go out as Matrix2D by default, as the reference posts
-// them (main.js indexes image[y][x]).  Progress/display messages (chunks,
-// markers, preview ImageData) are not emitted: they carry no results.
+// them (main.js indexes image[y][x]).  With {previews: true} the per-plane
+// preview messages are posted too, in the reference's order, with device-
+// made ImageData (RECEIVED_GAUSSIAN_BLURRED_IMAGE, _DIFFERENCE_OF_GAUSSIAN_
+// IMAGE, _CANDIDATE_KEYPOINT_BASE_IMAGE, candidate markers, _CANDIDATE_
+// KEYPOINT_IMAGE).  Not emitted: per-chunk previews (crops of the plane
+// previews) and low-contrast markers (only their count is kept on device).
 // ---------------------------------------------------------------------------
-export function createWorkerHandler(post, { matrix2d = true, device = 0 } = {}) {
+export function createWorkerHandler(post, { matrix2d = true, device = 0, previews = false } = {}) {
   return (e) => {
     const m = e && e.data !== undefined ? e.data : e;
     switch (m.type) {
-      case WorkerMessageTypes.COMPUTE_GAUSSIAN_SCALE_SPACE:
-        post({ type: WorkerMessageTypes.RECEIVED_GAUSSIAN_SCALE_SPACE,
-          scaleSpace: computeGaussianScaleSpace({ input_image: m.inputImage, number_of_octaves: m.numberOfOctaves,
-            scales_per_octave: m.scalesPerOctave, min_blur_level: m.minBlurLevel, assumed_blur: m.assumedBlur,
-            chunk_size: m.chunkSize, matrix2d, device }) });
+      case WorkerMessageTypes.COMPUTE_GAUSSIAN_SCALE_SPACE: {
+        const scaleSpace = computeGaussianScaleSpace({ input_image: m.inputImage, number_of_octaves: m.numberOfOctaves,
+          scales_per_octave: m.scalesPerOctave, min_blur_level: m.minBlurLevel, assumed_blur: m.assumedBlur,
+          chunk_size: m.chunkSize, matrix2d, device });
+        if (previews) {  // background.js:137-141 / :216-221
+          scaleSpace.forEach((oct, o) => oct.forEach((_, s) => post({
+            type: WorkerMessageTypes.RECEIVED_GAUSSIAN_BLURRED_IMAGE, imageData: planeImageData(scaleSpace, o, s), octave: o,
+          })));
+        }
+        post({ type: WorkerMessageTypes.RECEIVED_GAUSSIAN_SCALE_SPACE, scaleSpace });
         break;
-      case WorkerMessageTypes.COMPUTE_DIFFERENCE_OF_GAUSSIANS:
-        post({ type: WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIANS,
-          differenceOfGaussians: computeDifferenceOfGaussians(m.scaleSpace, 32, { device, matrix2d }) });
+      }
+      case WorkerMessageTypes.COMPUTE_DIFFERENCE_OF_GAUSSIANS: {
+        const dog = computeDifferenceOfGaussians(m.scaleSpace, 32, { device, matrix2d });
+        if (previews) {  // background.js:333-338
+          dog.forEach((oct, o) => oct.forEach((_, s) => post({
+            type: WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIAN_IMAGE,
+            imageData: planeImageData(dog, o, s, { mode: 'sampled' }), octave: o,
+          })));
+        }
+        post({ type: WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIANS, differenceOfGaussians: dog });
         break;
-      case WorkerMessageTypes.FIND_CANDIDATE_KEYPOINTS:
-        post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINTS,
-          candidateKeypoints: findCandidateKeypoints({ ...m, device }) });
+      }
+      case WorkerMessageTypes.FIND_CANDIDATE_KEYPOINTS: {
+        const candidateKeypoints = findCandidateKeypoints({ ...m, device });
+        if (previews) {  // background.js:380-429
+          const dogs = m.differenceOfGaussians;
+          candidateKeypoints.forEach((oct, o) => oct.forEach((sc) => {
+            post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINT_BASE_IMAGE,
+              imageData: planeImageData(dogs, o, sc.scaleLevel, { mode: 'sampled' }) });
+            for (const x of sc.localExtremas) {
+              post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINT_MARKER, x: x.x, y: x.y, isLowContrast: false });
+            }
+            post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINT_IMAGE, octave: o });
+          }));
+        }
+        post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINTS, candidateKeypoints });
         break;
+      }
       case WorkerMessageTypes.REFINE_CANDIDATE_KEYPOINTS:
         post({ type: WorkerMessageTypes.RECEIVED_REFINED_KEYPOINTS,
           refinedKeypoints: refineCandidateKeypoints({ ...m, device }) });

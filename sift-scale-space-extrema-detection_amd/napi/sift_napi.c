@@ -490,6 +490,112 @@ static napi_value js_abi_version(napi_env env, napi_callback_info info) {
   return v;
 }
 
+/* ---- image products (ABI >= 4): RGBA ImageData in, preview ImageData out ---- */
+static const uint8_t *rgba_data(napi_env env, napi_value v, size_t *len) {
+  const uint8_t *d = (const uint8_t *)typed_data(env, v, napi_uint8_clamped_array, len);
+  if (!d) d = (const uint8_t *)typed_data(env, v, napi_uint8_array, len);
+  return d;
+}
+
+static const uint8_t *rgba_args(napi_env env, napi_value *argv, int32_t *w, int32_t *h) {
+  size_t len = 0;
+  const uint8_t *rgba = rgba_data(env, argv[1], &len);
+  napi_get_value_int32(env, argv[2], w);
+  napi_get_value_int32(env, argv[3], h);
+  if (!rgba || *w <= 0 || *h <= 0 || (size_t)*w * (size_t)*h * 4 > len) {
+    napi_throw_type_error(env, NULL, "image data must be a Uint8ClampedArray of width*height RGBA pixels");
+    return NULL;
+  }
+  return rgba;
+}
+
+/* rgbaToGray(ctx, rgba, width, height, wantAlpha) -> {gray: Float32Array, alpha?: Float32Array} */
+static napi_value js_rgba_to_gray(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t w = 0, h = 0;
+  const uint8_t *rgba = rgba_args(env, argv, &w, &h);
+  if (!rgba) return NULL;
+  bool want_alpha = false;
+  if (argc > 4) napi_get_value_bool(env, argv[4], &want_alpha);
+  float *g = NULL, *a = NULL;
+  napi_value out, garr, aarr = NULL;
+  garr = make_typed(env, napi_float32_array, (size_t)w * h, 4, (void **)&g);
+  if (want_alpha) aarr = make_typed(env, napi_float32_array, (size_t)w * h, 4, (void **)&a);
+  int rc = sift_rgba_to_gray(ctx, rgba, w, h, (size_t)w * 4, g, a);
+  if (rc) return throw_sift(env, ctx, rc, "sift_rgba_to_gray");
+  napi_create_object(env, &out);
+  napi_set_named_property(env, out, "gray", garr);
+  if (aarr) napi_set_named_property(env, out, "alpha", aarr);
+  return out;
+}
+
+/* buildScaleSpaceRgba(ctx, rgba, width, height, params, Float64Array|null sigmas) */
+static napi_value js_build_rgba(napi_env env, napi_callback_info info) {
+  size_t argc = 6;
+  napi_value argv[6];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t w = 0, h = 0;
+  const uint8_t *rgba = rgba_args(env, argv, &w, &h);
+  if (!rgba) return NULL;
+  sift_params p;
+  read_params(env, argv[4], &p);
+  const double *sig = NULL;
+  if (argc > 5) sig = (const double *)typed_data(env, argv[5], napi_float64_array, NULL);
+  int rc = sift_build_scale_space_rgba(ctx, rgba, w, h, (size_t)w * 4, &p, sig);
+  if (rc) return throw_sift(env, ctx, rc, "sift_build_scale_space_rgba");
+  return NULL;
+}
+
+/* detectRgba(ctx, rgba, width, height, params) -> keypoints */
+static napi_value js_detect_rgba(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t w = 0, h = 0;
+  const uint8_t *rgba = rgba_args(env, argv, &w, &h);
+  if (!rgba) return NULL;
+  sift_params p;
+  read_params(env, argv[4], &p);
+  size_t n = 0;
+  int rc = sift_detect_rgba(ctx, rgba, w, h, (size_t)w * 4, &p, NULL, 0, &n);
+  if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_detect_rgba");
+  size_t sing = 0;
+  sift_last_counts(ctx, NULL, NULL, NULL, &sing, NULL);
+  return keypoints_to_js(env, ctx, n, sing);
+}
+
+/* planeImage(ctx, kind, octave, scale, mode, coefficient) -> Uint8ClampedArray(rows*cols*4) */
+static napi_value js_plane_image(napi_env env, napi_callback_info info) {
+  size_t argc = 6;
+  napi_value argv[6];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  int32_t kind = 0, o = 0, s = 0, mode = 0, rows = 0, cols = 0;
+  double coef = 1.0;
+  napi_get_value_int32(env, argv[1], &kind);
+  napi_get_value_int32(env, argv[2], &o);
+  napi_get_value_int32(env, argv[3], &s);
+  napi_get_value_int32(env, argv[4], &mode);
+  if (argc > 5) napi_get_value_double(env, argv[5], &coef);
+  int rc = sift_get_dims(ctx, o, &rows, &cols);
+  if (rc) return throw_sift(env, ctx, rc, "sift_get_dims");
+  uint8_t *dst;
+  const size_t bytes = (size_t)rows * cols * 4;
+  napi_value arr = make_typed(env, napi_uint8_clamped_array, bytes, 1, (void **)&dst);
+  rc = sift_plane_image(ctx, kind, o, s, mode, coef, dst, bytes);
+  if (rc) return throw_sift(env, ctx, rc, "sift_plane_image");
+  return arr;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"abiVersion", 0, js_abi_version, 0, 0, 0, napi_enumerable, 0},
@@ -507,6 +613,10 @@ static napi_value init(napi_env env, napi_value exports) {
       {"detect", 0, js_detect, 0, 0, 0, napi_enumerable, 0},
       {"detectAsync", 0, js_detect_async, 0, 0, 0, napi_enumerable, 0},
       {"counts", 0, js_counts, 0, 0, 0, napi_enumerable, 0},
+      {"rgbaToGray", 0, js_rgba_to_gray, 0, 0, 0, napi_enumerable, 0},
+      {"buildScaleSpaceRgba", 0, js_build_rgba, 0, 0, 0, napi_enumerable, 0},
+      {"detectRgba", 0, js_detect_rgba, 0, 0, 0, napi_enumerable, 0},
+      {"planeImage", 0, js_plane_image, 0, 0, 0, napi_enumerable, 0},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -34,6 +34,10 @@ AFTER_OCTAVE0 = 0
 AFTER_GAUSSIAN = 1
 AFTER_REFINEMENT = 2
 
+DISPLAY_PLAIN = 0
+DISPLAY_SIGMOID = 1
+DISPLAY_SAMPLED = 2
+
 # Exported symbols, exactly those include/sift_hip.h declares.
 ABI_SYMBOLS = (
     "sift_abi_version", "sift_params_default", "sift_ctx_create", "sift_ctx_destroy",
@@ -46,6 +50,8 @@ ABI_SYMBOLS = (
     "sift_detect_device_async", "sift_detect_wait", "sift_ctx_create_shared",
     "sift_next_seed", "sift_device_next_seed", "sift_detect_from_seed", "sift_detect_from_seed_device",
     "sift_keypoint_origins", "sift_set_row_origin", "sift_order_after",
+    "sift_rgba_to_gray", "sift_rgba_to_gray_device", "sift_build_scale_space_rgba", "sift_detect_rgba",
+    "sift_plane_image", "sift_plane_image_device",
 )
 
 
@@ -152,6 +158,14 @@ def lib():
         "sift_keypoint_origins": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int32), sz, szp]),
         "sift_set_row_origin": (ctypes.c_int, [vp, ctypes.c_int]),
         "sift_order_after": (ctypes.c_int, [vp, vp, ctypes.c_int]),
+        "sift_rgba_to_gray": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, fp, fp]),
+        "sift_rgba_to_gray_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, vp, vp]),
+        "sift_build_scale_space_rgba": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, dp]),
+        "sift_detect_rgba": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
+        "sift_plane_image": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_double, vp, sz]),
+        "sift_plane_image_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_double, vp, sz]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -334,6 +348,47 @@ class Context:
         self._check(rc, "sift_detect")
         self.params, self.width, self.height = params, W, H
         return self.keypoints()
+
+    # -- image products (ImageData in / preview ImageData out) ---------------
+    def rgba_to_gray(self, rgba, alpha=False):
+        """rgba: uint8 (H, W, 4) ImageData.data -> fp32 gray (H, W) [, alpha]
+        (image-utils.js:27-152 with the perceptual weights)."""
+        a = np.ascontiguousarray(rgba, dtype=np.uint8)
+        H, W = a.shape[0], a.shape[1]
+        g = np.empty((H, W), dtype=np.float32)
+        al = np.empty((H, W), dtype=np.float32) if alpha else None
+        self._check(self._L.sift_rgba_to_gray(self._h, a.ctypes.data_as(ctypes.c_void_p), W, H, W * 4,
+                                              g.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                              al.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if alpha else None),
+                    "sift_rgba_to_gray")
+        return (g, al) if alpha else g
+
+    def build_scale_space_rgba(self, rgba, params):
+        a = np.ascontiguousarray(rgba, dtype=np.uint8)
+        H, W = a.shape[0], a.shape[1]
+        self._check(self._L.sift_build_scale_space_rgba(self._h, a.ctypes.data_as(ctypes.c_void_p), W, H, W * 4,
+                                                        ctypes.byref(params), None), "sift_build_scale_space_rgba")
+        self.params, self.width, self.height = params, W, H
+
+    def detect_rgba(self, rgba, params, raise_singular=False):
+        a = np.ascontiguousarray(rgba, dtype=np.uint8)
+        H, W = a.shape[0], a.shape[1]
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect_rgba(self._h, a.ctypes.data_as(ctypes.c_void_p), W, H, W * 4,
+                                      ctypes.byref(params), None, 0, ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect_rgba")
+        self.params, self.width, self.height = params, W, H
+        return self.keypoints()
+
+    def plane_image(self, kind, octave, scale, mode=DISPLAY_PLAIN, coefficient=1.0):
+        """Preview ImageData (H, W, 4) uint8 of one plane (image-utils.js:171-217)."""
+        h, w = self.dims(octave)
+        out = np.empty((h, w, 4), dtype=np.uint8)
+        self._check(self._L.sift_plane_image(self._h, kind, octave, scale, mode, float(coefficient),
+                                             out.ctypes.data_as(ctypes.c_void_p), out.nbytes), "sift_plane_image")
+        return out
 
     def detect_device(self, d_ptr, width, height, params, stride=None, raise_singular=False):
         n = ctypes.c_size_t()

@@ -80,3 +80,51 @@ def test_js_stage_chain_matches_reference(name):
                           "received-candidate-keypoints", "received-refined-keypoints"]
     assert w["matrix2dRows"] == g.z["dims"][0][0]
     assert w["refined"] == g.refined.shape[0]
+
+
+@pytest.mark.gpu
+def test_js_image_products_match_reference():
+    """RGBA ImageData -> gray, plane previews and the preview messages of the
+    worker protocol through the JS module, against the fixtures the
+    reference's own image-utils.js / matrix2d.js produced."""
+    import image_products as ip
+    z = np.load(os.path.join(ROOT, "tests", "golden", "image_products.npz"))
+    H, W = z["rgba"].shape[:2]
+    with tempfile.TemporaryDirectory() as td:
+        z["rgba"].tofile(os.path.join(td, "rgba.u8"))
+        z["matrix_mod"].tofile(os.path.join(td, "m.f32"))
+        r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_image_products.mjs"),
+                            os.path.join(td, "rgba.u8"), str(W), str(H), os.path.join(td, "m.f32"),
+                            os.path.join(td, "o.json")], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        with open(os.path.join(td, "o.json")) as f:
+            out = json.load(f)
+    gray32 = z["gray"].astype(np.float32)
+    np.testing.assert_array_equal(np.array(out["gray"], np.float32).reshape(H, W), gray32)
+    np.testing.assert_array_equal(np.array(out["alpha"], np.float32).reshape(H, W), z["alpha"].astype(np.float32))
+    assert out["grayRows"] == H
+    np.testing.assert_array_equal(np.array(out["grayRow0"], np.float32), gray32[0])
+    for mode in ("plain", "sigmoid", "sampled"):
+        im = out["images"][mode]
+        assert (im["width"], im["height"], im["clamped"]) == (2 * W, 2 * H, True)
+        np.testing.assert_array_equal(np.array(im["data"], np.uint8).reshape(2 * H, 2 * W, 4), z["mod_" + mode])
+    assert len(out["detectRgba"]) == len(out["detectGray"]) > 0
+    assert out["detectRgba"] == out["detectGray"]
+    assert out["ssSample"] == out["ssSampleGray"]
+    w = out["worker"]
+    O, S = 3, 3
+    types = w["types"]
+    assert types[:O * (S + 3)] == ["received-gaussian-blurred-image"] * (O * (S + 3))
+    assert types[O * (S + 3)] == "received-gaussian-scale-space"
+    d0 = O * (S + 3) + 1
+    assert types[d0:d0 + O * (S + 2)] == ["received-difference-of-gaussian-image"] * (O * (S + 2))
+    assert types[d0 + O * (S + 2)] == "received-difference-of-gaussians"
+    f = types[d0 + O * (S + 2) + 1:]
+    assert f[-1] == "received-candidate-keypoints"
+    assert f.count("received-candidate-keypoint-base-image") == O * S
+    assert f.count("received-candidate-keypoint-image") == O * S
+    assert f.count("received-candidate-keypoint-marker") == w["candidates"] > 0
+    fp = w["firstGaussPreview"]
+    assert (fp["octave"], fp["w"], fp["h"]) == (0, 2 * W, 2 * H)
+    ref = ip.gray_image_data(np.array(out["gaussPlane00"], np.float64))
+    np.testing.assert_array_equal(np.array(fp["px"], np.uint8).reshape(4, 4), ref)
