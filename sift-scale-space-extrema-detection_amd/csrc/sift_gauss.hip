@@ -50,6 +50,8 @@
 #include "sift_common.h"
 #include "sift_kernels.h"
 
+#include <vector>
+
 namespace sift {
 
 constexpr int kGX = 64;              // tile columns
@@ -491,8 +493,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   // Scale group of this block (small octaves split their scales over
   // blockIdx.z for parallelism; a group recomputes the scale before it as
   // the DoG's L_{s-1}, without storing it).
-  const int G = gridDim.z, per = (P.NS + G - 1) / G;
-  const int s_begin = bz * per, s_end = min(P.NS, s_begin + per);
+  const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
   const int s_first = max(0, s_begin - 1);
   __syncthreads();  // staged region / zeroed strip visible to every wave
 
@@ -609,12 +610,67 @@ size_t gauss_lds_bytes(const Pyramid& P, int o) {
   return sizeof(double) * kGY * strip_stride(P, o) + staged_bytes(P, o);
 }
 
-// Scale groups per octave: enough blocks to fill 256 CUs several times.
+// Cost of one scale of a tile, in units of one fp64 tap per output of both
+// passes; the constant covers the strip round trip and the plane stores.
+static int scale_cost(const Octave& oc, int s) { return 2 * oc.rad[s] + 1 + 8; }
+
+// Split the NS scales of octave o into G contiguous groups (blockIdx.z) so
+// that the most expensive group -- which also recomputes the scale before it
+// as the DoG's L[s-1] -- is as cheap as possible (radii grow with s, so equal
+// scale counts would leave the last group with most of the work).  Returns
+// the max group cost; gb[0..G] are the group boundaries.
+static int split_scales(const Pyramid& P, int o, int G, int* gb) {
+  const Octave& oc = P.oct[o];
+  const int NS = P.NS;
+  // best[g][e]: min over splits of scales [0, e) into g groups of the max group cost
+  int best[kMaxScales + 1][kMaxScales + 1], cut[kMaxScales + 1][kMaxScales + 1];
+  auto cost = [&](int b, int e) {
+    int c = 0;
+    for (int s = std::max(0, b - 1); s < e; ++s) c += scale_cost(oc, s);
+    return c;
+  };
+  for (int e = 0; e <= NS; ++e) best[1][e] = cost(0, e), cut[1][e] = 0;
+  for (int g = 2; g <= G; ++g)
+    for (int e = g; e <= NS; ++e) {
+      best[g][e] = 1 << 30;
+      for (int b = g - 1; b < e; ++b) {
+        const int c = std::max(best[g - 1][b], cost(b, e));
+        if (c < best[g][e]) best[g][e] = c, cut[g][e] = b;
+      }
+    }
+  gb[G] = NS;
+  for (int g = G, e = NS; g >= 1; --g) {
+    gb[g - 1] = g > 1 ? cut[g][e] : 0;
+    e = gb[g - 1];
+  }
+  return best[G][NS];
+}
+
+// Scale groups per octave: small octaves split their scales so that enough
+// blocks fill the 256 CUs (octave 0 never splits: it is HBM-write bound and
+// every split recomputes a scale).  SIFT_GAUSS_GROUPS="g1,g2,..."
+// overrides the group count of octaves 1, 2, ... (experiments).
 static int scale_groups(const Pyramid& P, int o) {
+  static const std::vector<int> env = [] {
+    std::vector<int> v;
+    if (const char* e = std::getenv("SIFT_GAUSS_GROUPS"))
+      for (const char* p = e; *p;) {
+        v.push_back(std::atoi(p));
+        while (*p && *p != ',') ++p;
+        if (*p) ++p;
+      }
+    return v;
+  }();
+  if (o == 0) return 1;
+  if (o - 1 < (int)env.size() && env[o - 1] > 0) return std::min(env[o - 1], P.NS);
+  // Measured (4K, O=4, S=5; tools/gpu_groups.sh): every split adds the
+  // recomputed scale to the total work, so an octave splits only until it
+  // has ~1.5 blocks per CU -- 60x68 tiles: 1 group; 30x34: 1 (G=2: 116 us,
+  // G=4: 126-140 us, G=1: 103 us); 15x17: 2 (70.8 us; G=1 94 us, G=4 85 us).
   const Octave& oc = P.oct[o];
   const long long tiles = (long long)((oc.w + kGX - 1) / kGX) * ((oc.h + kGY - 1) / kGY);
   int g = 1;
-  while (g < P.NS / 2 && tiles * g < 2048) g *= 2;
+  while (g < P.NS && tiles * g < 400) ++g;
   return g;
 }
 
@@ -633,7 +689,9 @@ hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st)
 
 hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
   const Octave& oc = P.oct[L.o];
-  dim3 grid((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, scale_groups(P, L.o));
+  const int G = scale_groups(P, L.o);
+  split_scales(P, L.o, G, L.gb);
+  dim3 grid((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, G);
   const size_t lds = gauss_lds_bytes(P, L.o);
   static bool attr_set = false;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)

@@ -24,6 +24,7 @@ struct GaussLaunch {
   int vec;            // float4 plane stores are aligned
   int zero;           // strips need zeroing (generic-radius path present)
   int dbg;            // timing experiments (SIFT_GAUSS_DBG): bit 0 = no plane stores
+  int gb[kMaxScales + 1];  // scale groups (blockIdx.z): group g computes scales gb[g] .. gb[g+1]-1
 };
 
 constexpr int kXW = 62;      // output columns per extrema wave (lanes 1..62; lanes 0, 63 are halo)
