@@ -229,7 +229,12 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
   return x * q + min(x, r) + b / kXcd;
 }
 
-__global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const RefineLaunch L) {
+// EXACT: caller-supplied planes (the fp32 values are the data, no error
+// bound); one instantiation per mode keeps the register allocation of the
+// common fp32-plane path to its own code.
+template <bool EXACT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_refine_fast(const Pyramid P,
+                                                                                           const RefineLaunch L) {
   const int n = (int)min(*L.n, (unsigned)L.cap);
   const int nb = (n + 255) / 256;
   if ((int)blockIdx.x >= nb) return;  // whole block past the live slots
@@ -245,7 +250,7 @@ __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const Refi
     const long long plane = (long long)h * w;
     const float* __restrict__ D = P.dog + oc.dog_off;
     const double value = L.cand_val[i];
-    const double dval = L.exact_planes ? 0.0 : fabs(value) * 0x1p-24;
+    const double dval = EXACT ? 0.0 : fabs(value) * 0x1p-24;
     int status = kRefDiscard;
     double d[27];
     for (int it = 0; it < 5; ++it) {
@@ -256,15 +261,20 @@ __global__ __launch_bounds__(256) void k_refine_fast(const Pyramid P, const Refi
         for (int a = 0; a < 3; ++a)
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
+            // The 8 corners (k, a, c all != 1) enter neither the gradient nor
+            // the Hessian (sift.js:333-446): 19 loads, and the error bound is
+            // taken over the values that are used.
+            if (k != 1 && a != 1 && c != 1) {
+              d[k * 9 + a * 3 + c] = 0.0;
+              continue;
+            }
             const double v = (double)D[(s - 1 + k) * plane + (long long)(m - 1 + a) * w + (n - 1 + c)];
             d[k * 9 + a * 3 + c] = v;
             mx = fmax(mx, fabs(v));
           }
       // fp32 rounding of the fp64 value (<= |v| 2^-24) plus fp64 noise vs the reference.
-      const double delta = L.exact_planes ? 0.0 : mx * (0x1p-24 + 0x1p-40);
-      const StepOut R = L.exact_planes
-                            ? refine_step<false>(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4)
-                            : refine_step<true>(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4);
+      const double delta = EXACT ? 0.0 : mx * (0x1p-24 + 0x1p-40);
+      const StepOut R = refine_step<!EXACT>(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4);
       if (R.uncertain) {
         unc = true;
         for (int b = 0; b < 6; ++b)
@@ -376,7 +386,8 @@ __global__ void k_count_kp(const unsigned* __restrict__ pos, const unsigned* __r
 
 hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream_t st) {
   if (R.cap <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_refine_fast, dim3((R.cap + 255) / 256), dim3(256), 0, st, P, R);
+  if (R.exact_planes) hipLaunchKernelGGL(k_refine_fast<true>, dim3((R.cap + 255) / 256), dim3(256), 0, st, P, R);
+  else hipLaunchKernelGGL(k_refine_fast<false>, dim3((R.cap + 255) / 256), dim3(256), 0, st, P, R);
   return hipGetLastError();
 }
 
