@@ -102,7 +102,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=3,
                     help="detections in flight per GPU (one context each; the host settles image k while "
                          "image k+1 runs)")
-    ap.add_argument("--overlap", default="octave0", choices=["none", "octave0", "gaussian", "refinement", "full"],
+    ap.add_argument("--overlap", default="octave0",
+                    choices=["none", "octave0", "gaussian", "refinement", "full", "phased"],
                     help="how consecutive images overlap on the GPU: none = contexts share one stream; "
                          "octave0 / gaussian / refinement = own streams, image k+1 starts once image k has "
                          "passed that point (sift_order_after: software pipelining); full = own streams, "
@@ -152,10 +153,33 @@ def main():
 
     stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0, "gauss_oct0_ms": 0.0}
 
+    phased = args.overlap == "phased"
+    pend = [None]  # phased: the image whose extrema + refinement are not enqueued yet
+
     def launch(i):
+        c = ctxs[i % nin]
+        if phased:
+            # HBM-bound phases of consecutive images alternate: octave 0 of
+            # image i runs after image i-2's refinement and before image
+            # i-1's extrema scan; the small octaves (fp64 / TA bound) of one
+            # image overlap the extrema + refinement of the previous one.
+            if i >= 2:
+                c.order_after(ctxs[(i - 2) % nin], sift_amd.AFTER_REFINEMENT)
+            c.detect_begin_async(d_img.data_ptr(), W, H, params)
+            if pend[0] is not None:
+                p = ctxs[pend[0] % nin]
+                p.order_after(c, sift_amd.AFTER_OCTAVE0)
+                p.detect_end_async()
+            pend[0] = i
+            return
         if after is not None and i > 0 and nin > 1:
-            ctxs[i % nin].order_after(ctxs[(i - 1) % nin], after)
-        ctxs[i % nin].detect_device_async(d_img.data_ptr(), W, H, params)
+            c.order_after(ctxs[(i - 1) % nin], after)
+        c.detect_device_async(d_img.data_ptr(), W, H, params)
+
+    def flush():
+        if pend[0] is not None:
+            ctxs[pend[0] % nin].detect_end_async()
+            pend[0] = None
 
     def finish(i, acc):
         c = ctxs[i % nin]
@@ -171,6 +195,7 @@ def main():
     # Warm-up: every context settles its capacities synchronously first.
     for i in range(max(args.warmup, nin)):
         launch(i)
+        flush()
         finish(i, False)
     if dist is not None:
         dist.barrier()
@@ -183,6 +208,7 @@ def main():
         launch(i)
         if i >= nin - 1:
             n_total = finish(i - (nin - 1), True)
+    flush()
     for i in range(max(0, args.steps - (nin - 1)), args.steps):
         n_total = finish(i, True)
     for c in ctxs:

@@ -207,6 +207,16 @@ int sift_detect_device_async(struct sift_ctx *ctx, const float *d_img, int width
                              size_t stride_px, const sift_params *p);
 int sift_detect_wait(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out);
 
+/* The same detection in two phases (ABI version >= 4): _begin enqueues the
+ * Gaussian+DoG pass, _end the extrema scan and refinement; sift_detect_wait
+ * completes it.  Between the two, sift_order_after can hold the second
+ * phase back behind other contexts' work (bench.py --overlap phased: the
+ * next image's octave 0 runs before this image's extrema scan, so the
+ * HBM-bound phases of consecutive images alternate instead of contending). */
+int sift_detect_begin_async(struct sift_ctx *ctx, const float *d_img, int width, int height, size_t stride_px,
+                            const sift_params *p);
+int sift_detect_end_async(struct sift_ctx *ctx);
+
 /* Software pipelining of consecutive images on contexts with their own
  * streams (ABI version >= 3): the next work enqueued on ctx waits until
  * prev's last enqueued detection has passed `after`:

@@ -75,6 +75,7 @@ struct sift_ctx {
   bool scans_done = false;  // build_common already launched the extrema scans (side stream)
   bool counters_zeroed = false;  // extrema_prepare zeroed the refinement counters too
   bool detect_pending = false;   // sift_detect_device_async enqueued, sift_detect_wait not yet called
+  bool begin_pending = false;    // sift_detect_begin_async enqueued, sift_detect_end_async not yet called
   bool detect_host_img = false;
   ExtremaLaunch xl{};       // extrema launch state between prepare / scan / finish
   int o_first = 0;          // first octave of the pyramid in use (sift_detect_from_seed: > 0)
@@ -972,11 +973,22 @@ int sift_refine(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out, si
 
 // Enqueues one whole detection (Gaussian+DoG, extrema, refinement) without
 // waiting; detect_finish completes it.
-static int detect_enqueue(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
-                          size_t stride, const sift_params* p) {
+// Two phases: the Gaussian+DoG pass, then extrema + refinement (the caller
+// may order the second phase after other contexts' work in between).
+static int detect_begin(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H, size_t stride,
+                        const sift_params* p) {
   if (!ctx) return SIFT_E_ARG;
   int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, true);
   if (rc) return rc;
+  ctx->begin_pending = true;
+  ctx->detect_host_img = img_host != nullptr;
+  return SIFT_OK;
+}
+
+static int detect_end(sift_ctx* ctx) {
+  if (!ctx->begin_pending) return set_err(ctx, SIFT_E_STATE, "no detection begun (sift_detect_begin_async)");
+  ctx->begin_pending = false;
+  int rc;
   if (ctx->scans_done) {
     ctx->scans_done = false;
     rc = extrema_finish(ctx);
@@ -987,8 +999,13 @@ static int detect_enqueue(sift_ctx* ctx, const float* img_host, const float* img
   rc = refine_enqueue(ctx);
   if (rc) return rc;
   ctx->detect_pending = true;
-  ctx->detect_host_img = img_host != nullptr;
   return SIFT_OK;
+}
+
+static int detect_enqueue(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
+                          size_t stride, const sift_params* p) {
+  const int rc = detect_begin(ctx, img_host, img_dev, W, H, stride, p);
+  return rc ? rc : detect_end(ctx);
 }
 
 // One host synchronisation per image; a capacity overflow (first images)
@@ -1028,8 +1045,24 @@ int sift_detect_device_async(sift_ctx* ctx, const float* d_img, int width, int h
                              const sift_params* p) {
   if (!ctx) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
-  if (ctx->detect_pending) return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
+  if (ctx->detect_pending || ctx->begin_pending)
+    return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
   return detect_enqueue(ctx, nullptr, d_img, width, height, stride_px, p);
+}
+
+int sift_detect_begin_async(sift_ctx* ctx, const float* d_img, int width, int height, size_t stride_px,
+                            const sift_params* p) {
+  if (!ctx) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->detect_pending || ctx->begin_pending)
+    return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
+  return detect_begin(ctx, nullptr, d_img, width, height, stride_px, p);
+}
+
+int sift_detect_end_async(sift_ctx* ctx) {
+  if (!ctx) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  return detect_end(ctx);
 }
 
 int sift_detect_wait(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out) {

@@ -51,7 +51,7 @@ ABI_SYMBOLS = (
     "sift_next_seed", "sift_device_next_seed", "sift_detect_from_seed", "sift_detect_from_seed_device",
     "sift_keypoint_origins", "sift_set_row_origin", "sift_order_after",
     "sift_rgba_to_gray", "sift_rgba_to_gray_device", "sift_build_scale_space_rgba", "sift_detect_rgba",
-    "sift_plane_image", "sift_plane_image_device",
+    "sift_plane_image", "sift_plane_image_device", "sift_detect_begin_async", "sift_detect_end_async",
 )
 
 
@@ -143,6 +143,8 @@ def lib():
         "sift_detect_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_detect_device_async": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp]),
         "sift_detect_wait": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_detect_begin_async": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp]),
+        "sift_detect_end_async": (ctypes.c_int, [vp]),
         "sift_ctx_create_shared": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
         "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
         "sift_last_timings": (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
@@ -407,6 +409,17 @@ class Context:
                                                      int(stride or width), ctypes.byref(params)),
                     "sift_detect_device_async")
         self.params, self.width, self.height = params, width, height
+
+    def detect_begin_async(self, d_ptr, width, height, params, stride=None):
+        """Phase 1 of an asynchronous detection: the Gaussian+DoG pass."""
+        rc = self._L.sift_detect_begin_async(self._h, ctypes.c_void_p(int(d_ptr)), int(width), int(height),
+                                             int(stride or width), ctypes.byref(params))
+        self._check(rc, "sift_detect_begin_async")
+        self.params, self.width, self.height = params, width, height
+
+    def detect_end_async(self):
+        """Phase 2: extrema scan and refinement (complete with detect_wait)."""
+        self._check(self._L.sift_detect_end_async(self._h), "sift_detect_end_async")
 
     def order_after(self, prev, after=0):
         """Next work on this context waits until prev's last detection has

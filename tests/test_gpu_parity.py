@@ -248,6 +248,53 @@ def test_async_detect_matches_sync():
         hip.hipFree(d)
 
 
+def test_phased_detect_matches_sync():
+    """The two-phase API (sift_detect_begin_async / _end_async) in the bench's
+    phased schedule on three contexts with their own streams: each image's
+    extrema stage ordered after the next image's octave 0, each octave 0 after
+    the refinement two images back -- the same keypoints as the synchronous
+    call, for every image."""
+    img = np.ascontiguousarray(blob_image(640, 360, seed=43), dtype=np.float32)
+    p = sift_amd.make_params(4, 4)
+    hip, d = _device_copy(img)
+    try:
+        with sift_amd.Context(0) as r:
+            n_ref = r.detect_device(d.value, 640, 360, p)
+            ref = r.keypoints().tobytes()
+        ctxs = [sift_amd.Context(0) for _ in range(3)]
+        try:
+            with pytest.raises(sift_amd.SiftError):
+                ctxs[0].detect_end_async()  # nothing begun
+            pend = None
+            done = []
+            for i in range(7):
+                c = ctxs[i % 3]
+                if i >= 3:
+                    done.append((c.detect_wait(), c.keypoints().tobytes()))
+                if i >= 2:
+                    c.order_after(ctxs[(i - 2) % 3], sift_amd.AFTER_REFINEMENT)
+                c.detect_begin_async(d.value, 640, 360, p)
+                with pytest.raises(sift_amd.SiftError):
+                    c.detect_device_async(d.value, 640, 360, p)  # phase 1 in flight
+                if pend is not None:
+                    q = ctxs[pend % 3]
+                    q.order_after(c, sift_amd.AFTER_OCTAVE0)
+                    q.detect_end_async()
+                pend = i
+            ctxs[pend % 3].detect_end_async()
+            for i in range(4, 7):
+                c = ctxs[i % 3]
+                done.append((c.detect_wait(), c.keypoints().tobytes()))
+            assert len(done) == 7
+            for n, k in done:
+                assert n == n_ref and k == ref
+        finally:
+            for c in ctxs:
+                c.close()
+    finally:
+        hip.hipFree(d)
+
+
 # ---------------------------------------------------------------------------
 # Row-band shards of one image (SURVEY.md §8e cfg 5): crops of whole rows for
 # the leading octaves, the gathered fp64 base for the trailing ones.  The
