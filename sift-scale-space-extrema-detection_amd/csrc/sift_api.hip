@@ -55,6 +55,8 @@ struct sift_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = true;          // false: the stream of another context (sift_ctx_create_shared)
   hipStream_t side = nullptr;      // extrema scans of finished octaves, overlapping later octaves' Gaussians
+  hipStream_t hi = nullptr;        // high-priority stream for octave 0's Gaussian+DoG (SIFT_OCT0_PRIO=1)
+  hipEvent_t ev_hi_fork = nullptr, ev_hi_join = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_oct[kMaxOctaves]{};
   std::string err;
   sift_params p{};
@@ -207,6 +209,17 @@ static int ctx_create(int device, sift_ctx* share, sift_ctx** out) {
       return SIFT_E_HIP;
     }
   }
+  if (std::getenv("SIFT_OCT0_PRIO") && std::atoi(std::getenv("SIFT_OCT0_PRIO"))) {
+    int lo = 0, hi = 0;
+    bool ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+              hipStreamCreateWithPriority(&ctx->hi, hipStreamNonBlocking, hi) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->ev_hi_fork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->ev_hi_join, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      (void)sift_ctx_destroy(ctx);
+      return SIFT_E_HIP;
+    }
+  }
   *out = ctx;
   return SIFT_OK;
 }
@@ -238,6 +251,9 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->hi) (void)hipStreamSynchronize(ctx->hi), (void)hipStreamDestroy(ctx->hi);
+  if (ctx->ev_hi_fork) (void)hipEventDestroy(ctx->ev_hi_fork);
+  if (ctx->ev_hi_join) (void)hipEventDestroy(ctx->ev_hi_join);
   if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SIFT_OK;
@@ -433,8 +449,18 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off
                                 : (xseed ? ctx->xseed.as<double>() : nullptr);
     L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : (xseed ? ctx->xseed_w : 0);
-    HIPCHK(launch_gauss_dog(P, L, ctx->stream));
-    if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+    hipStream_t ls = ctx->stream;
+    if (o == 0 && ctx->hi) {  // octave 0 on the high-priority stream, joined back
+      HIPCHK(hipEventRecord(ctx->ev_hi_fork, ctx->stream));
+      HIPCHK(hipStreamWaitEvent(ctx->hi, ctx->ev_hi_fork, 0));
+      ls = ctx->hi;
+    }
+    HIPCHK(launch_gauss_dog(P, L, ls));
+    if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ls));
+    if (ls != ctx->stream) {
+      HIPCHK(hipEventRecord(ctx->ev_hi_join, ls));
+      HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_hi_join, 0));
+    }
     if (overlap) {
       HIPCHK(hipEventRecord(ctx->ev_oct[o], ctx->stream));
       HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_oct[o], 0));

@@ -28,7 +28,10 @@ struct GaussLaunch {
 };
 
 constexpr int kXW = 62;      // output columns per extrema wave (lanes 1..62; lanes 0, 63 are halo)
-constexpr int kXRows = 30;   // centre rows per extrema wave (multiple of 3)
+#ifndef SIFT_XROWS
+#define SIFT_XROWS 30
+#endif
+constexpr int kXRows = SIFT_XROWS;  // centre rows per extrema wave (multiple of 3)
 constexpr int kXMaxGroup = 5;// scales per extrema wave (S > 5 splits the scales into groups)
 
 // One launch scans every octave: unit u (one wave) = (octave, strip of kXRows
