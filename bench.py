@@ -99,6 +99,9 @@ def main():
     ap.add_argument("--scales", type=int, default=5)
     ap.add_argument("--skip-gauss-planes", action="store_true",
                     help="keypoints-only mode: do not materialise the Gaussian planes")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="independent images per GPU per step (BASELINE cfg 4: --width 1920 --height 1080 "
+                         "--batch 8 on 8 GPUs = 64 images per step)")
     ap.add_argument("--inflight", type=int, default=3,
                     help="detections in flight per GPU (one context each; the host settles image k while "
                          "image k+1 runs)")
@@ -204,12 +207,13 @@ def main():
         c.synchronize()
     t0 = time.perf_counter()
     n_total = 0
-    for i in range(args.steps):  # image i is enqueued before image i-(nin-1) is settled
+    NI = args.steps * max(1, args.batch)  # images in the timed region
+    for i in range(NI):  # image i is enqueued before image i-(nin-1) is settled
         launch(i)
         if i >= nin - 1:
             n_total = finish(i - (nin - 1), True)
     flush()
-    for i in range(max(0, args.steps - (nin - 1)), args.steps):
+    for i in range(max(0, NI - (nin - 1)), NI):
         n_total = finish(i, True)
     for c in ctxs:
         c.synchronize()
@@ -233,13 +237,14 @@ def main():
         for k in iso:
             iso[k] += t[k] / n_iso
     K = args.steps
+    Bt = max(1, args.batch)
     ms_per_step = elapsed / K * 1e3
-    value = world * W * H / (elapsed / K) / 1e6
-    counts = ctxs[(args.steps - 1) % nin].counts()
+    value = world * Bt * W * H / (elapsed / K) / 1e6
+    counts = ctxs[(NI - 1) % nin].counts()
 
     if rank == 0:
-        gauss_ms = stage["gauss_dog_ms"] / K
-        oct0_ms = stage["gauss_oct0_ms"] / K
+        gauss_ms = stage["gauss_dog_ms"] / NI
+        oct0_ms = stage["gauss_oct0_ms"] / NI
         B = alg_bytes(W, H, O, S, args.skip_gauss_planes)
         B0 = oct0_bytes(W, H, S, args.skip_gauss_planes)
         achieved = B0 / (oct0_ms * 1e-3) / 1e9
@@ -260,17 +265,19 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": "%dx%d gray f32 image per GPU per step, %d octaves x %d scales, "
+                "workload": "%s%dx%d gray f32 image%s per GPU per step, %d octaves x %d scales, "
                             "Gaussian+DoG+extrema+refine (keypoints out)%s" %
-                            (W, H, O, S, ", Gaussian planes not materialised" if args.skip_gauss_planes else ""),
+                            ("%d x " % Bt if Bt > 1 else "", W, H, "s" if Bt > 1 else "", O, S,
+                             ", Gaussian planes not materialised" if args.skip_gauss_planes else ""),
                 "width": W, "height": H, "octaves": O, "scales_per_octave": S,
-                "images_per_gpu": 1, "global_batch": world, "inflight_per_gpu": nin,
+                "images_per_gpu": Bt, "global_batch": world * Bt, "inflight_per_gpu": nin,
                 "streams_per_gpu": nin if own else 1,
                 "overlap": args.overlap,
-                "parallelism": "dp%d (one image per GPU, RCCL keypoint all-gather)" % world if world > 1 else "single GPU",
+                "parallelism": ("dp%d (%d image%s per GPU, RCCL keypoint all-gather)" % (world, Bt, "s" if Bt > 1 else "")
+                                if world > 1 else "single GPU"),
                 "planes": "fp32 out, fp64 accumulation/seeds",
             },
-            "stages_ms": {k: round(v / K, 4) for k, v in stage.items()},
+            "stages_ms": {k: round(v / NI, 4) for k, v in stage.items()},
             "keypoints": counts["keypoints"],
             "candidates": counts["candidates"],
             "keypoints_all_ranks": n_total,
