@@ -320,6 +320,14 @@ int sift_plane_image(struct sift_ctx *ctx, int kind, int octave, int scale, int 
 int sift_plane_image_device(struct sift_ctx *ctx, int kind, int octave, int scale, int mode,
                             double coefficient, uint8_t *d_rgba, size_t cap_bytes);
 
+/* Device-resident forms for a shard driver that keeps everything on the GPU
+ * (ABI version >= 4): the origins of sift_keypoint_origins decoded on
+ * device into caller device memory (4 int32 per keypoint), and rows
+ * [row_begin, row_end) of the octave-(num_octaves) base into caller device
+ * memory.  Both complete before return. */
+int sift_copy_keypoint_origins_device(struct sift_ctx *ctx, int32_t *d_dst, size_t cap, size_t *n_out);
+int sift_copy_next_seed_device(struct sift_ctx *ctx, double *d_dst, size_t cap, int row_begin, int row_end);
+
 /* Wait for all work queued on ctx's stream. */
 int sift_synchronize(struct sift_ctx *ctx);
 

@@ -1322,6 +1322,32 @@ int sift_set_row_origin(sift_ctx* ctx, int input_row0) {
   return SIFT_OK;
 }
 
+int sift_copy_keypoint_origins_device(sift_ctx* ctx, int32_t* d_dst, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->has_origins) return set_err(ctx, SIFT_E_STATE, "no keypoint origins (SIFT_F_KEYPOINT_ORIGINS)");
+  if (n_out) *n_out = ctx->n_kp;
+  if (!d_dst || ctx->n_kp == 0) return SIFT_OK;
+  if (cap < 4 * ctx->n_kp) return set_err(ctx, SIFT_E_CAPACITY, "destination too small (4 per keypoint)");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(launch_decode_origins(ctx->P, ctx->kp_key.as<unsigned>(), (int)ctx->n_kp, d_dst, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
+int sift_copy_next_seed_device(sift_ctx* ctx, double* d_dst, size_t cap, int row_begin, int row_end) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->has_xseed) return set_err(ctx, SIFT_E_STATE, "no next-octave base (SIFT_F_EXPORT_NEXT_SEED)");
+  if (row_begin < 0 || row_end > ctx->xseed_h || row_begin > row_end) return set_err(ctx, SIFT_E_ARG, "bad row range");
+  const size_t n = (size_t)(row_end - row_begin) * ctx->xseed_w;
+  if (!d_dst || n == 0) return SIFT_OK;
+  if (cap < n) return set_err(ctx, SIFT_E_CAPACITY, "destination too small");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(d_dst, ctx->xseed.as<double>() + (size_t)row_begin * ctx->xseed_w, n * sizeof(double),
+                        hipMemcpyDeviceToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
+}
+
 int sift_keypoint_origins(sift_ctx* ctx, int32_t* out, size_t cap, size_t* n_out) {
   if (!ctx) return SIFT_E_ARG;
   if (!ctx->has_origins) return set_err(ctx, SIFT_E_STATE, "no keypoint origins (SIFT_F_KEYPOINT_ORIGINS)");

@@ -128,6 +128,9 @@ hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, con
 
 size_t exact_lds_bytes(const Pyramid& P);
 
+// keys -> 4 int32 per keypoint: octave, scale, whole-image octave row (row0 applied), x.
+hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st);
+
 // Image products either side of the path (sift_image.hip).
 // gray/alpha rows are dense (w floats); alpha may be nullptr.
 hipError_t launch_rgba_to_gray(const unsigned char* rgba, size_t stride_bytes, int w, int h, float* gray,

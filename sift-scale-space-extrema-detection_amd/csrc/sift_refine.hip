@@ -384,6 +384,25 @@ __global__ void k_count_kp(const unsigned* __restrict__ pos, const unsigned* __r
   *out = m ? pos[m - 1] + keep[m - 1] : 0u;
 }
 
+// Candidate key of each keypoint -> (octave, scale, whole-image row, x).
+__global__ __launch_bounds__(256) void k_decode_origins(const Pyramid P, const unsigned* __restrict__ keys, int n,
+                                                        int32_t* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int o, s, y, x;
+  decode_key(P, keys[i], o, s, y, x);
+  out[4 * i + 0] = o;
+  out[4 * i + 1] = s;
+  out[4 * i + 2] = y + ((P.row0 * 2) >> o);
+  out[4 * i + 3] = x;
+}
+
+hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_decode_origins, dim3((n + 255) / 256), dim3(256), 0, st, P, keys, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream_t st) {
   if (R.cap <= 0) return hipSuccess;
   if (R.exact_planes) hipLaunchKernelGGL(k_refine_fast<true>, dim3((R.cap + 255) / 256), dim3(256), 0, st, P, R);

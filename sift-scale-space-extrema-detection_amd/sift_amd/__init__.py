@@ -52,6 +52,7 @@ ABI_SYMBOLS = (
     "sift_keypoint_origins", "sift_set_row_origin", "sift_order_after",
     "sift_rgba_to_gray", "sift_rgba_to_gray_device", "sift_build_scale_space_rgba", "sift_detect_rgba",
     "sift_plane_image", "sift_plane_image_device", "sift_detect_begin_async", "sift_detect_end_async",
+    "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device",
 )
 
 
@@ -145,6 +146,8 @@ def lib():
         "sift_detect_wait": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_detect_begin_async": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp]),
         "sift_detect_end_async": (ctypes.c_int, [vp]),
+        "sift_copy_keypoint_origins_device": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_copy_next_seed_device": (ctypes.c_int, [vp, vp, sz, ctypes.c_int, ctypes.c_int]),
         "sift_ctx_create_shared": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
         "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
         "sift_last_timings": (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
@@ -421,6 +424,22 @@ class Context:
         """Phase 2: extrema scan and refinement (complete with detect_wait)."""
         self._check(self._L.sift_detect_end_async(self._h), "sift_detect_end_async")
 
+    def copy_keypoint_origins_device(self, d_dst, cap):
+        """Decoded origins (4 int32 per keypoint) into device memory; returns the count."""
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_copy_keypoint_origins_device(self._h, ctypes.c_void_p(int(d_dst)), int(cap),
+                                                               ctypes.byref(n)), "sift_copy_keypoint_origins_device")
+        return int(n.value)
+
+    def copy_next_seed_device(self, d_dst, cap, row_begin, row_end):
+        self._check(self._L.sift_copy_next_seed_device(self._h, ctypes.c_void_p(int(d_dst)), int(cap),
+                                                        int(row_begin), int(row_end)), "sift_copy_next_seed_device")
+
+    def next_seed_dims(self):
+        r, c = ctypes.c_int(), ctypes.c_int()
+        self._check(self._L.sift_next_seed(self._h, None, 0, ctypes.byref(r), ctypes.byref(c)), "sift_next_seed")
+        return r.value, c.value
+
     def order_after(self, prev, after=0):
         """Next work on this context waits until prev's last detection has
         passed `after` (AFTER_OCTAVE0 / AFTER_GAUSSIAN / AFTER_REFINEMENT,
@@ -458,6 +477,19 @@ class Context:
         self._check(rc, "sift_detect_from_seed")
         self.params, self.width, self.height = params, width, height
         return self.keypoints()
+
+    def detect_from_seed_device(self, d_seed, octave_first, width, height, params, raise_singular=False):
+        """detect_from_seed with the fp64 base in device memory; keypoints stay
+        on device (returns the count)."""
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect_from_seed_device(self._h, int(octave_first), ctypes.c_void_p(int(d_seed)),
+                                                  int(width), int(height), ctypes.byref(params), None, 0,
+                                                  ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect_from_seed_device")
+        self.params, self.width, self.height = params, width, height
+        return n.value
 
     def set_row_origin(self, input_row0):
         """Input row of the first row of the following images (a row-band crop)."""

@@ -219,3 +219,177 @@ def detect_sharded(ctx, img, params, group=None, max_overhead=0.5):
     gathered = [None] * world
     dist.all_gather_object(gathered, mine, group=group)
     return merge([p for g in gathered for p in g]), plan
+
+
+# ---------------------------------------------------------------------------
+# Device-resident driver: the image, the crops (pointer offsets into the
+# whole image), the keypoints, their origins and the base rows stay in HBM;
+# owned-row filtering and the ordered merge are torch ops on the device, the
+# gathers are all_gather_into_tensor over RCCL.  Records are 48-byte
+# sift_keypoint rows of a uint8 tensor.
+# ---------------------------------------------------------------------------
+REC = KEYPOINT_DTYPE.itemsize
+
+
+def _seed_rows(plan, r):
+    """Rows [s0, s1) of shard r's octave-(K+1) base that it owns, in its crop's rows."""
+    lo, hi = plan.bands[r]
+    c0, c1 = plan.crops[r]
+    K = plan.K
+    h_crop = octave_dims(plan.width, c1 - c0, K + 2)[K + 1][0]
+    s0 = (lo >> K) - (c0 >> K)
+    s1 = h_crop if r == len(plan.bands) - 1 else (hi >> K) - (c0 >> K)
+    return s0, s1
+
+
+def _device_lists(ctx, n, torch, dev):
+    kp = torch.empty((max(n, 1), REC), dtype=torch.uint8, device=dev)
+    org = torch.empty((max(n, 1), 4), dtype=torch.int32, device=dev)
+    if n:
+        ctx.copy_keypoints_device(kp.data_ptr(), n)
+        ctx.copy_keypoint_origins_device(org.data_ptr(), 4 * n)
+    return kp[:n], org[:n]
+
+
+def run_shard_device(ctx, d_img, params, plan, r):
+    """Shard r from the whole image `d_img` (H x W fp32 torch tensor on ctx's
+    device): (keypoints uint8 [n, 48], origins int32 [n, 4], owned base rows
+    fp64 [rows, cols] or None), all on the device."""
+    import torch
+    dev = d_img.device
+    lo, hi = plan.bands[r]
+    c0, c1 = plan.crops[r]
+    K = plan.K
+    last = r == len(plan.bands) - 1
+    W = plan.width
+    flags = params.flags | F_KEYPOINT_ORIGINS | (F_EXPORT_NEXT_SEED if plan.has_tail else 0)
+    p = make_params(K + 1, params.scales_per_octave, params.min_blur, params.assumed_blur,
+                    params.min_interpixel_distance, flags)
+    ctx.set_row_origin(c0)
+    try:
+        n = ctx.detect_device(d_img.data_ptr() + c0 * W * 4, W, c1 - c0, p)
+        kp, org = _device_lists(ctx, n, torch, dev)
+        part = None
+        if plan.has_tail:
+            s0, s1 = _seed_rows(plan, r)
+            rows, cols = ctx.next_seed_dims()
+            part = torch.empty((s1 - s0, cols), dtype=torch.float64, device=dev)
+            ctx.copy_next_seed_device(part.data_ptr(), part.numel(), s0, s1)
+    finally:
+        ctx.set_row_origin(0)
+    o = org[:, 0].long()
+    y = org[:, 2].long()
+    lo_o = torch.where(o == 0, torch.full_like(o, 2 * lo), lo >> (o - 1).clamp(min=0))
+    keep = y >= lo_o
+    if not last:
+        hi_o = torch.where(o == 0, torch.full_like(o, 2 * hi), hi >> (o - 1).clamp(min=0))
+        keep &= y < hi_o
+    return kp[keep], org[keep], part
+
+
+def run_tail_device(ctx, d_base, params, plan):
+    """Octaves K+1..O-1 from the gathered base (fp64 torch tensor on the device)."""
+    import torch
+    p = make_params(params.num_octaves, params.scales_per_octave, params.min_blur, params.assumed_blur,
+                    params.min_interpixel_distance, params.flags | F_KEYPOINT_ORIGINS)
+    h, w = octave_dims(plan.width, plan.height, plan.num_octaves)[plan.K + 1]
+    if tuple(d_base.shape) != (h, w):
+        raise ValueError("gathered base %s != octave %d dims %s" % (tuple(d_base.shape), plan.K + 1, (h, w)))
+    n = ctx.detect_from_seed_device(d_base.data_ptr(), plan.K + 1, plan.width, plan.height, p)
+    return _device_lists(ctx, n, torch, d_base.device)
+
+
+def merge_device(kps, orgs):
+    """Ordered merge on the device: sort by candidate (octave, scale, y, x)."""
+    import torch
+    kp = torch.cat(kps)
+    org = torch.cat(orgs).long()
+    key = ((org[:, 0] * 16 + org[:, 1]) * (1 << 20) + org[:, 2]) * (1 << 20) + org[:, 3]
+    return kp[torch.argsort(key)]
+
+
+def _sync(t):
+    if t.is_cuda:
+        import torch
+        torch.cuda.synchronize(t.device)
+
+
+def detect_sharded_device_local(ctx, d_img, params, n_shards, max_overhead=0.5, timer=None):
+    """All shards on one device in turn (device-resident): the sharded
+    algorithm without the collectives.  Returns (uint8 [n, 48] keypoints on
+    the device, plan).  timer: optional dict of per-part seconds."""
+    import torch
+    H, W = d_img.shape
+    plan = plan_bands(W, H, params, n_shards, max_overhead)
+    kps, orgs, seeds = [], [], []
+    for r in range(len(plan.bands)):
+        t0 = time.perf_counter()
+        kp, org, seed = run_shard_device(ctx, d_img, params, plan, r)
+        _sync(d_img)
+        _tick(timer, "shard%d" % r, t0)
+        kps.append(kp)
+        orgs.append(org)
+        seeds.append(seed)
+    if plan.has_tail:
+        t0 = time.perf_counter()
+        kp, org = run_tail_device(ctx, torch.cat(seeds), params, plan)
+        _sync(d_img)
+        _tick(timer, "tail", t0)
+        kps.append(kp)
+        orgs.append(org)
+    t0 = time.perf_counter()
+    out = merge_device(kps, orgs)
+    _sync(d_img)
+    _tick(timer, "merge", t0)
+    return out, plan
+
+
+def gather_rows(t, counts, group=None):
+    """all_gather of a ragged first dimension (every rank knows all counts):
+    pad to the largest, all_gather_into_tensor, strip.  Returns the rank-order
+    concatenation."""
+    import torch
+    import torch.distributed as dist
+    world = len(counts)
+    m = max(max(counts), 1)
+    send = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    send[:t.shape[0]] = t
+    recv = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    return torch.cat([recv[i * m:i * m + counts[i]] for i in range(world)])
+
+
+def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5):
+    """One shard per rank, device-resident (RCCL with the nccl backend):
+    gather the owned base rows (the tail runs on rank 0), then the keypoints
+    and their origins; every rank returns the whole image's keypoints
+    (uint8 [n, 48] on its device) in the reference's order."""
+    import torch
+    import torch.distributed as dist
+    H, W = d_img.shape
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = d_img.device
+    plan = plan_bands(W, H, params, world, max_overhead)
+    nb = len(plan.bands)
+    if rank < nb:
+        kp, org, seed = run_shard_device(ctx, d_img, params, plan, rank)
+    else:
+        kp = torch.zeros((0, REC), dtype=torch.uint8, device=dev)
+        org = torch.zeros((0, 4), dtype=torch.int32, device=dev)
+        seed = None
+    if plan.has_tail:
+        cols = octave_dims(W, H, plan.num_octaves)[plan.K + 1][1]
+        rows = [(lambda a: a[1] - a[0])(_seed_rows(plan, r)) if r < nb else 0 for r in range(world)]
+        mine = seed if seed is not None else torch.zeros((0, cols), dtype=torch.float64, device=dev)
+        base = gather_rows(mine, rows, group)
+        if rank == 0:
+            tk, to = run_tail_device(ctx, base, params, plan)
+            kp, org = torch.cat([kp, tk]), torch.cat([org, to])
+    cnt = torch.tensor([kp.shape[0]], dtype=torch.int64, device=dev)
+    cnts = torch.zeros(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(cnts, cnt, group=group)
+    counts = [int(c) for c in cnts.tolist()]
+    all_kp = gather_rows(kp, counts, group)
+    all_org = gather_rows(org, counts, group)
+    return merge_device([all_kp], [all_org]), plan

@@ -17,6 +17,16 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
+    # torch (its own bundled HIP runtime) must initialise the device before
+    # libsift_hip.so's runtime does, as bench.py does: the other order leaves
+    # torch with "No HIP GPUs are available" for the tests that hand torch
+    # device tensors to the library.
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     import sift_amd
     ctx = sift_amd.Context(0)
     yield ctx

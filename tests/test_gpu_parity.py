@@ -319,6 +319,40 @@ def test_row_band_shards_match_whole_image(gpu_ctx, W, H, O, S, n, overhead):
         np.testing.assert_array_equal(merged[f], whole[f], err_msg=f)
 
 
+@pytest.mark.parametrize("W,H,O,S,n,overhead", [
+    (480, 360, 4, 3, 3, 0.5),
+    (640, 600, 5, 3, 4, 4.0),
+    (512, 520, 4, 5, 5, 0.05),
+    (1920, 1080, 5, 5, 8, 0.5),
+])
+def test_row_band_shards_device_resident(gpu_ctx, W, H, O, S, n, overhead):
+    """The device-resident driver (crops as pointer offsets, on-device origin
+    decoding, owned-row filtering, base-row copies and ordered merge) gives
+    the whole-image keypoints bit for bit, and the decoded device origins
+    equal the host-decoded ones."""
+    import torch
+    from sift_amd.shard import detect_sharded_device_local
+    img = blob_image(W, H, seed=11 + n)
+    p = sift_amd.make_params(O, S)
+    whole = gpu_ctx.detect(img, p).copy()
+    d_img = torch.from_numpy(img).to("cuda:0")
+    merged, plan = detect_sharded_device_local(gpu_ctx, d_img, p, n, max_overhead=overhead)
+    got = np.frombuffer(merged.cpu().numpy().tobytes(), dtype=sift_amd.KEYPOINT_DTYPE)
+    assert len(plan.bands) == n
+    assert got.shape == whole.shape, (got.shape, whole.shape, plan)
+    assert got.tobytes() == whole.tobytes()
+    pk = sift_amd.make_params(O, S, flags=sift_amd.F_KEYPOINT_ORIGINS)
+    gpu_ctx.set_row_origin(2 ** (O - 1) * 3)
+    try:
+        n_kp = gpu_ctx.detect_device(d_img.data_ptr(), W, H, pk)
+        host = gpu_ctx.keypoint_origins()
+        dev = torch.empty((max(n_kp, 1), 4), dtype=torch.int32, device="cuda:0")
+        assert gpu_ctx.copy_keypoint_origins_device(dev.data_ptr(), 4 * n_kp) == n_kp
+    finally:
+        gpu_ctx.set_row_origin(0)
+    np.testing.assert_array_equal(dev[:n_kp].cpu().numpy(), host)
+
+
 def test_keypoint_origins_and_next_seed(gpu_ctx):
     """Origins are the candidates of the keypoints; the exported base equals
     the base a deeper run builds (its octave-O Gaussian scale 0)."""

@@ -157,3 +157,87 @@ def test_merge_orders_by_candidate():
     a, b = perm[: len(perm) // 2], perm[len(perm) // 2:]
     m = merge([(kp[a], org[a]), (kp[b], org[b]), (kp[:0], org[:0])])
     assert m.tobytes() == kp.tobytes()
+
+
+class FakeDeviceCtx(FakeCtx):
+    """The device-resident interface of sift_amd.Context over CPU tensors:
+    'device pointers' are host addresses of CPU tensors (ctypes.memmove)."""
+
+    def detect_device(self, ptr, W, h, p):
+        self.detect(np.zeros((h, W), np.float32), p)
+        return int(self.last.sum())
+
+    def copy_keypoints_device(self, ptr, cap):
+        import ctypes
+        b = self.kp[self.last].tobytes()
+        ctypes.memmove(ptr, b, len(b))
+        return int(self.last.sum())
+
+    def copy_keypoint_origins_device(self, ptr, cap):
+        import ctypes
+        b = np.ascontiguousarray(self.org[self.last], dtype=np.int32).tobytes()
+        ctypes.memmove(ptr, b, len(b))
+        return int(self.last.sum())
+
+    def next_seed_dims(self):
+        b = self.next_seed()
+        return b.shape
+
+    def copy_next_seed_device(self, ptr, cap, s0, s1):
+        import ctypes
+        b = np.ascontiguousarray(self.next_seed()[s0:s1]).tobytes()
+        ctypes.memmove(ptr, b, len(b))
+
+    def detect_from_seed_device(self, ptr, o_first, W, H, p):
+        import ctypes
+        h, w = octave_dims(W, H, self.O)[o_first]
+        base = np.frombuffer((ctypes.c_double * (h * w)).from_address(ptr), dtype=np.float64).reshape(h, w)
+        self.detect_from_seed(base.copy(), o_first, W, H, p)
+        return int(self.last.sum())
+
+
+@pytest.mark.parametrize("shape,n", [((480, 360, 4, 3), 3), ((7680, 4320, 6, 5), 8), ((640, 600, 5, 3), 1)])
+def test_device_driver_local_with_stand_in(shape, n):
+    """detect_sharded_device_local (torch ops for filtering and the ordered
+    merge) reproduces the whole image with a stand-in context on CPU tensors."""
+    import torch
+    W, H, O, S = shape
+    ctx = FakeDeviceCtx(W, H, O)
+    from sift_amd.shard import detect_sharded_device_local
+    merged, plan = detect_sharded_device_local(ctx, torch.zeros((H, W), dtype=torch.float32),
+                                               sift_amd.make_params(O, S), n)
+    assert merged.numpy().tobytes() == ctx.kp.tobytes()
+
+
+def _worker_device(rank, world, port, shape, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        from sift_amd.shard import detect_sharded_device
+        W, H, O, S = shape
+        ctx = FakeDeviceCtx(W, H, O)
+        merged, plan = detect_sharded_device(ctx, torch.zeros((H, W), dtype=torch.float32),
+                                             sift_amd.make_params(O, S))
+        out_q.put((rank, merged.numpy().tobytes(), ctx.kp.tobytes(), plan.K))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shape", [(480, 360, 4, 3), (7680, 4320, 6, 5)])
+def test_detect_sharded_device_gathers_world2(shape):
+    """The device-resident driver's gathers (all_gather_into_tensor of the
+    padded base rows, counts, records and origins) over gloo, world size 2."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_device, args=(r, world, port, shape, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, merged, truth, K in res:
+        assert merged == truth, "rank %d: merged shards differ from the whole image" % rank
