@@ -89,19 +89,41 @@ def plan_bands(width, height, params, n_shards, max_overhead=0.5):
         return BandPlan(width, height, O, O - 1, bands, [(0, height)])
     band_min = min(hi - lo for lo, hi in bands)
     radii = octave_radii(params)
-    K = 0
+    k_max = 0
     for k in range(O - 1, -1, -1):
         if margin_rows(radii, k) <= max_overhead * band_min:
-            K = k
+            k_max = k
             break
-    M = margin_rows(radii, K)
-    step = 2 ** K
-    crops = []
-    for lo, hi in bands:
-        c0 = max(0, lo - M) // step * step
-        c1 = min(height, hi + M)
-        crops.append((c0, c1))
-    return BandPlan(width, height, O, K, bands, crops)
+
+    def crops_for(K):
+        M = margin_rows(radii, K)
+        step = 2 ** K
+        return [(max(0, lo - M) // step * step, min(height, hi + M)) for lo, hi in bands]
+
+    # Among the splits the margin allows, the one with the shortest critical
+    # path: the largest crop's octaves 0..K, then the tail K+1..O-1 on one
+    # device (shard_cost).  Deeper splits shorten the tail but grow the crops.
+    cost = [octave_cost(width, height, radii, o) for o in range(O)]
+    best = None
+    for K in range(k_max, -1, -1):
+        crops = crops_for(K)
+        frac = max(c1 - c0 for c0, c1 in crops) / float(height)
+        t = frac * sum(cost[:K + 1]) + sum(cost[K + 1:])
+        if best is None or t < best[0]:
+            best = (t, K, crops)
+    return BandPlan(width, height, O, best[1], bands, best[2])
+
+
+# Cost model of one octave of a whole W x H input, in seconds on one MI355X:
+# per octave pixel, both separable passes of every scale (2r+1 fp64 taps
+# each) plus the stores, the extrema scan and the refinement (~90 tap
+# equivalents), at ~1.06e-13 s per tap-pixel, plus ~30 us of launch and tail
+# latency per octave (fitted to the 4K per-octave kernel times of DESIGN.md
+# section 6).
+def octave_cost(width, height, radii, o):
+    h, w = octave_dims(width, height, o + 1)[o]
+    taps = sum(2 * (2 * r + 1) for r in radii[o]) + 90
+    return h * w * taps * 1.06e-13 + 30e-6
 
 
 def _owned(org, lo, hi, last):
@@ -300,7 +322,10 @@ def run_tail_device(ctx, d_base, params, plan):
 
 
 def merge_device(kps, orgs):
-    """Ordered merge on the device: sort by candidate (octave, scale, y, x)."""
+    """Ordered merge on the device: one argsort of the 48-bit candidate key
+    (octave, scale, y, x).  (A sort-free merge -- per (octave, scale) block
+    offsets from bincounts and prefix sums, one scatter -- measured slower at
+    8K, 1.02-1.08 vs 0.89 ms: a dozen small torch ops and a host sync.)"""
     import torch
     kp = torch.cat(kps)
     org = torch.cat(orgs).long()

@@ -241,3 +241,23 @@ def test_detect_sharded_device_gathers_world2(shape):
         p.join(timeout=60)
     for rank, merged, truth, K in res:
         assert merged == truth, "rank %d: merged shards differ from the whole image" % rank
+
+
+def test_merge_device_equals_sort():
+    """The sort-free device merge equals a full sort by candidate on ragged
+    parts that own disjoint row ranges per (octave, scale), plus a tail."""
+    import torch
+    from sift_amd.shard import merge_device
+    kp, org = _fake_truth(640, 600, 5, n=300, seed=4)
+    # split octaves 0..2 into 3 row bands, octaves 3..4 = tail
+    parts = []
+    for lo, hi in ((0, 100), (100, 250), (250, 10 ** 6)):
+        sel = (org[:, 0] <= 2) & (org[:, 2] >= lo) & (org[:, 2] < hi)
+        parts.append(sel)
+    parts.append(org[:, 0] > 2)
+    kps = [torch.from_numpy(np.frombuffer(kp[m].tobytes(), np.uint8).reshape(-1, 48).copy()) for m in parts]
+    orgs = [torch.from_numpy(org[m].copy()) for m in parts]
+    kps.insert(1, kps[0][:0])
+    orgs.insert(1, orgs[0][:0])
+    out = merge_device(kps, orgs)
+    assert out.numpy().tobytes() == kp.tobytes()
