@@ -25,6 +25,10 @@
 #include "sift_exact.h"
 #include "sift_kernels.h"
 
+#ifndef SIFT_XLOAD_AUX
+#define SIFT_XLOAD_AUX 0  // cache-policy bits of the scan's DoG loads (gfx950: 1 sc0, 2 nt, 16 sc1)
+#endif
+
 namespace sift {
 
 __device__ __forceinline__ unsigned lane_prefix(unsigned long long mask) {
@@ -89,7 +93,8 @@ __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int
 #pragma unroll
   for (int q = 0; q < NP; ++q)
     dst[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                           U.rsrc, (int)U.xoff, (int)(rofs + (unsigned)q * U.plane_bytes), 0));
+                                           U.rsrc, (int)U.xoff, (int)(rofs + (unsigned)q * U.plane_bytes),
+                                           SIFT_XLOAD_AUX));
 }
 
 template <int NP, int K>
