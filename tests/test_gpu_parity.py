@@ -177,6 +177,32 @@ def test_flat_image_has_no_keypoints(gpu_ctx):
     assert kp.shape[0] == 0 and gpu_ctx.counts()["candidates"] == 0
 
 
+@pytest.mark.parametrize("W,H,O,S", [(1, 1, 1, 3), (3, 2, 2, 3), (7, 1, 3, 2), (1, 9, 4, 3), (5, 5, 5, 5),
+                                     (2, 64, 3, 3), (4, 300, 3, 3), (300, 3, 3, 3), (6, 6, 2, 3)])
+def test_degenerate_sizes_match_oracle(gpu_ctx, W, H, O, S):
+    """Images down to 1 x 1 and one-pixel-wide strips, octaves down to 1 x 1:
+    every Gaussian / DoG plane within fp32 rounding of the oracle, and the
+    same (here: empty or tiny) candidate and keypoint lists."""
+    rng = np.random.default_rng(W * 31 + H)
+    img = (rng.integers(0, 4097, size=(H, W)) / 4096.0).astype(np.float32)
+    p = sift_amd.make_params(O, S)
+    kp = gpu_ctx.detect(img, p)
+    r = orc.OracleRun(img, orc.make_params(O, S), orc.CONV_SEPARABLE)
+    for o, (h, w) in enumerate(r.dims):
+        assert gpu_ctx.dims(o) == (h, w)
+        for s in range(S + 3):
+            np.testing.assert_allclose(gpu_ctx.plane(sift_amd.PLANE_GAUSS, o, s), r.gauss[o][s], rtol=2 ** -23,
+                                       atol=1e-12)
+    check_candidates(gpu_ctx.candidates(), r.candidates())
+    check_keypoints(kp, r.refined)
+
+
+def test_empty_image_is_rejected(gpu_ctx):
+    with pytest.raises(sift_amd.SiftError) as e:
+        gpu_ctx.detect(np.zeros((0, 5), np.float32), sift_amd.make_params(2, 3))
+    assert e.value.code == sift_amd.SIFT_E_ARG
+
+
 def test_detect_is_deterministic(gpu_ctx):
     img = blob_image(512, 384, seed=23)
     p = sift_amd.make_params(4, 5)
