@@ -32,6 +32,12 @@ K is the deepest octave whose margin fits the thinnest band (scaled by
 Exchange: the base rows and the keypoint lists are gathered once each
 (all_gather over RCCL/xGMI with torch.distributed, or in-process for a single
 device driving several shards).  No other data crosses devices.
+
+Two drivers: detect_sharded / detect_sharded_local work on host arrays
+(all_gather_object); detect_sharded_device / detect_sharded_device_local keep
+the image, keypoints, origins and base rows in HBM (crops are pointer
+offsets, all_gather_into_tensor, merge by argsort on the device).  K is
+chosen by a cost model of the critical path (octave_cost).
 """
 import math
 import time
