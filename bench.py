@@ -73,19 +73,36 @@ def load_traffic(cfg_key):
     return None, None
 
 
-def cpu_baseline(img_full, O, S, sample_w, sample_h):
-    """The oracle's reference-faithful 2D-kernel port, 1 thread, on a crop."""
+def cpu_baseline(img_full, O, S, sample_w, sample_h, threads=1):
+    """The oracle's reference-faithful 2D-kernel port on a crop, with `threads`
+    threads in its blur loops (1 = the scalar port)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     crop = img_full[:sample_h, :sample_w].copy()
     p = orc.make_params(O, S)
-    t0 = time.perf_counter()
-    nk, nc = orc.detect_count(crop, p, orc.CONV_2D)
-    dt = time.perf_counter() - t0
-    return {"value": round(sample_w * sample_h / dt / 1e6, 6), "unit": "Mpix/s", "cores": 1, "kind": "port",
+    orc.set_threads(threads)
+    try:
+        t0 = time.perf_counter()
+        nk, nc = orc.detect_count(crop, p, orc.CONV_2D)
+        dt = time.perf_counter() - t0
+    finally:
+        orc.set_threads(1)
+    return {"value": round(sample_w * sample_h / dt / 1e6, 6), "unit": "Mpix/s", "cores": threads, "kind": "port",
             "sample": "%dx%d crop of the same synthetic image, %d oct x %d scales, G+DoG+extrema+refine, "
-                      "reference 2D-kernel algorithm restated in C (oracle/sift_oracle.c CONV_2D), "
-                      "%.1f s, %d keypoints" % (sample_w, sample_h, O, S, dt, nk)}
+                      "reference 2D-kernel algorithm restated in C (oracle/sift_oracle.c CONV_2D%s), "
+                      "%.1f s, %d keypoints" % (sample_w, sample_h, O, S,
+                                                ", blur loops over %d OpenMP threads" % threads if threads > 1
+                                                else "", dt, nk)}
+
+
+def host_cores():
+    """CPU threads this process may use (the GPU box's share is 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(n, cap))
 
 
 def main():
@@ -317,10 +334,14 @@ def main():
                 },
             },
             "cpu_baseline": None,
+            "cpu_baseline_all_cores": None,
         }
         if world == 1 and not args.no_cpu_baseline:
             sw, sh = (int(v) for v in args.cpu_sample.split("x"))
             out["cpu_baseline"] = cpu_baseline(img, O, S, min(sw, W), min(sh, H))
+            nt = host_cores()
+            if nt > 1:  # the port on 1 core and on all the cores this process may use
+                out["cpu_baseline_all_cores"] = cpu_baseline(img, O, S, min(sw, W), min(sh, H), threads=nt)
         print(json.dumps(out), flush=True)
     for c in reversed(ctxs):
         c.close()

@@ -45,6 +45,8 @@ def lib():
         L.oracle_octave_dims.restype = ctypes.c_long
         L.oracle_octave_dims.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ip]
         L.oracle_schedule.argtypes = [pp, dp, dp]
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_set_threads.restype = None
         L.oracle_scale_space.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int,
                                          pp, ctypes.c_int, dp]
         L.oracle_dog.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, dp]
@@ -151,3 +153,8 @@ def detect_count(img, p, mode=CONV_2D):
     nk = lib().oracle_detect_count(_ptr(img, ctypes.c_float), W, H, ctypes.byref(p), mode,
                                    ctypes.byref(nc))
     return int(nk), int(nc.value)
+
+
+def set_threads(n):
+    """Threads of the oracle's blur loops (results are identical for any n)."""
+    lib().oracle_set_threads(int(n))

@@ -10,10 +10,20 @@
 
 #include <float.h>
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdlib.h>
 #include <string.h>
 
 /* Math.round: nearest integer, ties toward +infinity (exact for |x|<2^52). */
+/* Threads of the blur loops (oracle_set_threads; default 1 = the scalar
+ * port the CPU baseline is quoted on).  Each output pixel is the same sum in
+ * the same order whatever the thread count. */
+static int g_threads = 1;
+
+void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+
 static double js_round(double x) {
   double f = floor(x);
   return (x - f >= 0.5) ? f + 1.0 : f;
@@ -75,13 +85,43 @@ static double *build_kernel_2d(double sig, int *size) {
 
 static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+/* Rows [y0, y1) of fn's output; with g_threads > 1 the rows are split into
+ * contiguous ranges, one per thread.  The hot loops live in the range
+ * functions, so the 1-thread path runs exactly the scalar code. */
+typedef void (*row_fn)(const void *ctx, int y0, int y1);
+
+static void for_rows(row_fn fn, const void *ctx, int h) {
+  if (g_threads <= 1 || h < 2) {
+    fn(ctx, 0, h);
+    return;
+  }
+#pragma omp parallel num_threads(g_threads)
+  {
+#ifdef _OPENMP
+    int t = omp_get_thread_num(), nt = omp_get_num_threads();
+#else
+    int t = 0, nt = 1;
+#endif
+    int y0 = (int)((long)h * t / nt), y1 = (int)((long)h * (t + 1) / nt);
+    fn(ctx, y0, y1);
+  }
+}
+
+typedef struct {
+  const double *in;
+  double *out;
+  const double *K;
+  int h, w, ks, shift;
+} blur2d_ctx;
+
 /* sift.js:72-149 SIFT_blurMatrix2DChunk over the whole plane: i (kernel row)
  * offsets x, j offsets y, clamped reads, x-offset outer / y-offset inner. */
-static void blur_2d(const double *in, double *out, int h, int w, double sig) {
-  int ks;
-  double *K = build_kernel_2d(sig, &ks);
-  int shift = ks / 2;
-  for (int y = 0; y < h; y++)
+static void blur_2d_rows(const void *vc, int y0, int y1) {
+  const blur2d_ctx *c = (const blur2d_ctx *)vc;
+  const double *in = c->in, *K = c->K;
+  double *out = c->out;
+  const int h = c->h, w = c->w, ks = c->ks, shift = c->shift;
+  for (int y = y0; y < y1; y++)
     for (int x = 0; x < w; x++) {
       double acc = 0.0;
       for (int i = 0; i < ks; i++) {
@@ -93,7 +133,43 @@ static void blur_2d(const double *in, double *out, int h, int w, double sig) {
       }
       out[(long)y * w + x] = acc;
     }
+}
+
+static void blur_2d(const double *in, double *out, int h, int w, double sig) {
+  int ks;
+  double *K = build_kernel_2d(sig, &ks);
+  blur2d_ctx c = {in, out, K, h, w, ks, ks / 2};
+  for_rows(blur_2d_rows, &c, h);
   free(K);
+}
+
+typedef struct {
+  const double *in;
+  double *out;
+  const double *wt;
+  int h, w, r, n;
+} sep_ctx;
+
+static void sep_rows_h(const void *vc, int y0, int y1) {
+  const sep_ctx *c = (const sep_ctx *)vc;
+  const int w = c->w, r = c->r, n = c->n;
+  for (int y = y0; y < y1; y++)
+    for (int x = 0; x < w; x++) {
+      double acc = 0.0;
+      for (int i = 0; i < n; i++) acc += c->wt[i] * c->in[(long)y * w + clampi(x + i - r, 0, w - 1)];
+      c->out[(long)y * w + x] = acc;
+    }
+}
+
+static void sep_rows_v(const void *vc, int y0, int y1) {
+  const sep_ctx *c = (const sep_ctx *)vc;
+  const int h = c->h, w = c->w, r = c->r, n = c->n;
+  for (int y = y0; y < y1; y++)
+    for (int x = 0; x < w; x++) {
+      double acc = 0.0;
+      for (int j = 0; j < n; j++) acc += c->wt[j] * c->in[(long)clampi(y + j - r, 0, h - 1) * w + x];
+      c->out[(long)y * w + x] = acc;
+    }
 }
 
 /* Same operator, separable: w(i) = g1(i)/sum g1 with g1 = exp((i^2/s^2)*-0.5),
@@ -110,18 +186,10 @@ static void blur_sep(const double *in, double *out, int h, int w, double sig) {
   }
   for (int i = 0; i < n; i++) wt[i] /= sum;
   double *tmp = (double *)malloc(sizeof(double) * (size_t)h * w);
-  for (int y = 0; y < h; y++)
-    for (int x = 0; x < w; x++) {
-      double acc = 0.0;
-      for (int i = 0; i < n; i++) acc += wt[i] * in[(long)y * w + clampi(x + i - r, 0, w - 1)];
-      tmp[(long)y * w + x] = acc;
-    }
-  for (int y = 0; y < h; y++)
-    for (int x = 0; x < w; x++) {
-      double acc = 0.0;
-      for (int j = 0; j < n; j++) acc += wt[j] * tmp[(long)clampi(y + j - r, 0, h - 1) * w + x];
-      out[(long)y * w + x] = acc;
-    }
+  sep_ctx ch = {in, tmp, wt, h, w, r, n};
+  for_rows(sep_rows_h, &ch, h);
+  sep_ctx cv = {tmp, out, wt, h, w, r, n};
+  for_rows(sep_rows_v, &cv, h);
   free(tmp);
   free(wt);
 }

@@ -33,6 +33,9 @@ long oracle_octave_dims(int W, int H, int O, int *dims);
 /* blur[o*(S+3)+s] = blurLevel, sigma[o*(S+3)+s] = offset sigma (0 = copy). */
 void oracle_schedule(const oracle_params *p, double *blur, double *sigma);
 
+/* Threads of the blur loops (default 1). */
+void oracle_set_threads(int n);
+
 /* Gaussian scale space, (S+3) planes per octave. mode: ORACLE_CONV_*. */
 int oracle_scale_space(const float *img, int W, int H, const oracle_params *p,
                        int mode, double *gauss);
