@@ -22,6 +22,8 @@
 // fp32 comparison decides the fp64 one unless two fp32 values tie; ties and
 // |v| within rounding of 0.8*thr go to a short list that k_exact_extrema
 // re-decides from an fp64 pointwise recompute (sift_exact.h).
+#include <cstdlib>
+
 #include "sift_exact.h"
 #include "sift_kernels.h"
 
@@ -372,7 +374,11 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
   // 32-bit buffer offsets cover one scale group's planes
   const int np = std::min(P.S, kXMaxGroup) + 2;
   if (4.0 * np * (double)P.oct[0].h * P.oct[0].w >= 4294967296.0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_extrema, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), 0, st, P, L);
+  // SIFT_XLDS (bytes, experiments): unused dynamic LDS per block, capping the
+  // scan's blocks per CU (160 KiB / SIFT_XLDS) to leave CUs to other images.
+  static const int xlds = [] { const char* e = std::getenv("SIFT_XLDS"); return e ? std::atoi(e) : 0; }();
+  if (xlds > 65536) (void)hipFuncSetAttribute((const void*)k_extrema, hipFuncAttributeMaxDynamicSharedMemorySize, xlds);
+  hipLaunchKernelGGL(k_extrema, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), xlds, st, P, L);
   return hipGetLastError();
 }
 
