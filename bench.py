@@ -31,8 +31,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sift-scale-space-extrema-detection_amd"))
 
-METRIC = "Mpix/s through Gaussian+DoG+extrema, 4K img, 4 oct × 5 scales; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def metric_name(W, H, O, S, batch=1):
+    """BASELINE.json's metric string, with this run's image size and pyramid
+    (3840x2160 is the baseline's "4K")."""
+    size = "4K" if (W, H) == (3840, 2160) else "%dx%d" % (W, H)
+    return "Mpix/s through Gaussian+DoG+extrema, %s img%s, %d oct × %d scales; %% HBM roofline" % (
+        size, " x %d per GPU" % batch if batch > 1 else "", O, S)
 
 
 def octave_dims(W, H, O):
@@ -54,22 +61,41 @@ def alg_bytes(W, H, O, S, skip_gauss):
     return b
 
 
+def octave_bytes(W, H, O, S, skip_gauss):
+    """Algorithmic bytes of each octave's Gaussian+DoG launch (they sum to
+    alg_bytes): its planes written in fp32, plus the input read for octave 0
+    (skip_gauss: the fp64 seed of octave o >= 1 is written instead of its
+    Gaussian planes)."""
+    out = []
+    for o, (h, w) in enumerate(octave_dims(W, H, O)):
+        b = 4 * h * w * (S + 2) + (4 * W * H if o == 0 else 0)
+        b += (8 * h * w if o > 0 else 0) if skip_gauss else 4 * h * w * (S + 3)
+        out.append(b)
+    return out
+
+
 def oct0_bytes(W, H, S, skip_gauss):
     """Algorithmic bytes of octave 0's Gaussian+DoG launch."""
-    h, w = octave_dims(W, H, 1)[0]
-    return 4 * W * H + 4 * h * w * (S + 2) + (0 if skip_gauss else 4 * h * w * (S + 3))
+    return octave_bytes(W, H, 1, S, skip_gauss)[0]
 
 
-def load_traffic(cfg_key):
-    """Per-launch HBM bytes of octave 0's k_gauss_dog from a committed PMC summary."""
+def extrema_bytes(W, H, O, S):
+    """Algorithmic bytes of the extrema scan: every DoG plane read once."""
+    return sum(4 * h * w * (S + 2) for h, w in octave_dims(W, H, O))
+
+
+def load_traffic(cfg_key, field="hbm_bytes_per_launch"):
+    """HBM bytes per launch (or per pass: field="pass_hbm_bytes") from the
+    newest committed PMC summary for this configuration (profiles/*pmc*.json,
+    tools/pmc_launches.py / tools/pmc_traffic.py)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("config_key") == cfg_key and d.get("hbm_bytes_per_launch"):
-            return float(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+        if d.get("config_key") == cfg_key and d.get(field):
+            return float(d[field]), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -101,7 +127,10 @@ def host_cores():
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    try:  # OpenMP allows a list ("8,2"): the first level is what one process gets
+        cap = int(os.environ.get("OMP_NUM_THREADS", "16").split(",")[0])
+    except ValueError:
+        cap = 16
     return max(1, min(n, cap))
 
 
@@ -172,6 +201,7 @@ def main():
         gather = KeypointGather("cuda:%d" % dev)
 
     stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0, "gauss_oct0_ms": 0.0}
+    oct_ms = [0.0] * O
 
     phased = args.overlap == "phased"
     pend = [None]  # phased: the image whose extrema + refinement are not enqueued yet
@@ -210,6 +240,8 @@ def main():
             t = c.timings()
             for k in stage:
                 stage[k] += t[k]
+            for o, v in enumerate(c.octave_timings()):
+                oct_ms[o] += v
         return n
 
     # Warm-up: every context settles its capacities synchronously first.
@@ -245,14 +277,17 @@ def main():
     # After the timed region: the same detection alone (one image in flight,
     # nothing overlapping), so the kernel's isolated duration is on record
     # beside its pipelined one.
-    iso = {"gauss_dog_ms": 0.0, "gauss_oct0_ms": 0.0}
-    n_iso = 5
+    iso = {"gauss_dog_ms": 0.0, "gauss_oct0_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0}
+    iso_oct = [0.0] * O
+    n_iso = 10
     for _ in range(n_iso):
         ctx.detect_device_async(d_img.data_ptr(), W, H, params)
         ctx.detect_wait()
         t = ctx.timings()
         for k in iso:
             iso[k] += t[k] / n_iso
+        for o, v in enumerate(ctx.octave_timings()):
+            iso_oct[o] += v / n_iso
     K = args.steps
     Bt = max(1, args.batch)
     ms_per_step = elapsed / K * 1e3
@@ -263,13 +298,19 @@ def main():
         gauss_ms = stage["gauss_dog_ms"] / NI
         oct0_ms = stage["gauss_oct0_ms"] / NI
         B = alg_bytes(W, H, O, S, args.skip_gauss_planes)
-        B0 = oct0_bytes(W, H, S, args.skip_gauss_planes)
-        achieved = B0 / (oct0_ms * 1e-3) / 1e9
-        stage_achieved = B / (gauss_ms * 1e-3) / 1e9
+        Bo = octave_bytes(W, H, O, S, args.skip_gauss_planes)
+        B0 = Bo[0]
+        gbs = lambda b, ms: b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         cfg_key = "%dx%d_o%d_s%d%s" % (W, H, O, S, "_nogauss" if args.skip_gauss_planes else "")
-        traffic, traffic_src = load_traffic(cfg_key)
+        pass_traffic, pass_src = load_traffic(cfg_key, "pass_hbm_bytes")
+        oct0_traffic, oct0_src = load_traffic(cfg_key)
+        pipelined_note = ("pipelined: %d images in flight on %d streams, each launch's window includes "
+                          "waiting for CUs held by the other images' kernels" % (nin, nin)
+                          if own and nin > 1 else "one image at a time")
+        B_x = extrema_bytes(W, H, O, S)
+        iso_pass = iso["gauss_dog_ms"]
         out = {
-            "metric": METRIC,
+            "metric": metric_name(W, H, O, S, Bt),
             "value": round(value, 3),
             "unit": "Mpix/s",
             "n_gpus": world,
@@ -300,37 +341,50 @@ def main():
             "keypoints_all_ranks": n_total,
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_gauss_dog (octave 0)",
-                "achieved": round(achieved, 1),
+                "kernel": "Gaussian+DoG pass: k_gauss_dog, %d launches (one per octave)" % O,
+                "achieved": round(gbs(B, iso_pass), 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "alg_bytes_per_launch": B0,
-                "alg_bytes_formula": ("4WH + 4P_0(S+2)" if args.skip_gauss_planes
-                                      else "4WH + 4P_0(S+3) + 4P_0(S+2)"),
-                "launch_ms": round(oct0_ms, 5),
-                "measured": ("HIP events around the launch on its stream, averaged over the timed region%s" %
-                             ("" if args.overlap == "none" or nin == 1 else
-                              " (pipelined: includes waiting for CUs held by the previous image's kernels)")),
-                "isolated": {
-                    "what": "same launch, one image in flight, nothing overlapping (%d images after the timed "
-                            "region)" % n_iso,
-                    "launch_ms": round(iso["gauss_oct0_ms"], 5),
-                    "achieved": round(B0 / (iso["gauss_oct0_ms"] * 1e-3) / 1e9, 1),
-                    "frac": round(B0 / (iso["gauss_oct0_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "stage_ms": round(iso["gauss_dog_ms"], 5),
-                    "stage_frac": round(B / (iso["gauss_dog_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                },
-                "stage": {
-                    "what": "whole Gaussian+DoG pass, %d launches (one per octave)" % O,
-                    "alg_bytes": B,
-                    "alg_bytes_formula": ("4WH + sum_o 4P_o(S+2) + sum_{o>=1} 8P_o" if args.skip_gauss_planes
-                                          else "4WH + sum_o 4P_o(S+3) + sum_o 4P_o(S+2)"),
+                "frac": round(gbs(B, iso_pass) / HBM_PEAK_GBS, 4),
+                "traffic": pass_traffic,
+                "traffic_source": pass_src,
+                "alg_bytes_per_launch": B,
+                "alg_bytes_formula": ("4WH + sum_o 4P_o(S+2) + sum_{o>=1} 8P_o" if args.skip_gauss_planes
+                                      else "4WH + sum_o 4P_o(S+3) + sum_o 4P_o(S+2)"),
+                "launch_ms": round(iso_pass, 5),
+                "measured": ("HIP events on the context stream around the pass (first octave launch to the end "
+                             "of the last), one image at a time, averaged over %d images run right after the "
+                             "timed region (SURVEY.md §8d's north-star quantity; the pipelined window of the "
+                             "timed region is `pipelined`)" % n_iso),
+                "per_octave": [
+                    {"octave": o, "plane": list(octave_dims(W, H, O)[o]), "alg_bytes": Bo[o],
+                     "iso_ms": round(iso_oct[o], 5), "iso_frac": round(gbs(Bo[o], iso_oct[o]) / HBM_PEAK_GBS, 4),
+                     "pipelined_ms": round(oct_ms[o] / NI, 5)}
+                    for o in range(O)],
+                "pipelined": {
+                    "what": "the same pass inside the timed region (%s), HIP events, averaged over %d images" %
+                            (pipelined_note, NI),
                     "ms": round(gauss_ms, 5),
-                    "achieved": round(stage_achieved, 1),
-                    "frac": round(stage_achieved / HBM_PEAK_GBS, 4),
+                    "achieved": round(gbs(B, gauss_ms), 1),
+                    "frac": round(gbs(B, gauss_ms) / HBM_PEAK_GBS, 4),
+                },
+                "octave0": {
+                    "what": "octave 0's k_gauss_dog launch alone (HBM-store bound)",
+                    "alg_bytes": B0,
+                    "iso_ms": round(iso["gauss_oct0_ms"], 5),
+                    "iso_frac": round(gbs(B0, iso["gauss_oct0_ms"]) / HBM_PEAK_GBS, 4),
+                    "pipelined_ms": round(oct0_ms, 5),
+                    "pipelined_frac": round(gbs(B0, oct0_ms) / HBM_PEAK_GBS, 4),
+                    "traffic": oct0_traffic,
+                    "traffic_source": oct0_src,
+                },
+                "extrema_stage": {
+                    "what": "extrema stage (scan of every DoG plane + ordered emission + exact re-decisions), "
+                            "one image at a time",
+                    "alg_bytes": B_x,
+                    "alg_bytes_formula": "sum_o 4P_o(S+2)",
+                    "iso_ms": round(iso["extrema_ms"], 5),
+                    "iso_frac": round(gbs(B_x, iso["extrema_ms"]) / HBM_PEAK_GBS, 4),
                 },
             },
             "cpu_baseline": None,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 4
+#define SIFT_ABI_VERSION 5
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -231,6 +231,12 @@ enum { SIFT_AFTER_OCTAVE0 = 0, SIFT_AFTER_GAUSSIAN = 1, SIFT_AFTER_REFINEMENT = 
 int sift_order_after(struct sift_ctx *ctx, const struct sift_ctx *prev, int after);
 
 int sift_last_timings(struct sift_ctx *ctx, sift_timings *t);
+
+/* Per-octave Gaussian+DoG launch times of the last build / detection, ms
+ * (ABI version >= 5): ms[o] for o < *n_octaves (0 for octaves not built).
+ * Launch o is timed from the end of launch o-1 on the same stream, so with
+ * other streams' work overlapping it includes the wait for CUs. */
+int sift_last_octave_timings(struct sift_ctx *ctx, double *ms, int cap, int *n_octaves);
 
 /* Device-to-device copy of the last keypoints into caller device memory
  * (e.g. an RCCL all-gather send buffer), ordered on ctx's stream and

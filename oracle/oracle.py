@@ -52,6 +52,9 @@ def lib():
         L.oracle_dog.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, dp]
         L.oracle_find_extrema.restype = ctypes.c_long
         L.oracle_find_extrema.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, ip, dp, ctypes.c_long, lp]
+        L.oracle_find_extrema_ex.restype = ctypes.c_long
+        L.oracle_find_extrema_ex.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, ip, dp, ctypes.c_long, ip, dp,
+                                             ctypes.c_long, lp]
         L.oracle_refine.restype = ctypes.c_long
         L.oracle_refine.argtypes = [pp, ctypes.c_int, ctypes.c_int, dp, ip, dp, ctypes.c_long, dp,
                                     ctypes.c_long, lp]
@@ -98,7 +101,10 @@ def split_pyramid(flat, dims, per_octave):
 class OracleRun:
     """Full oracle pipeline on one image; keeps flat fp64 pyramids."""
 
-    def __init__(self, img, p, mode=CONV_SEPARABLE):
+    def __init__(self, img, p, mode=CONV_SEPARABLE, threads=1, keep_gauss=True):
+        """threads: OpenMP threads of the blur loops and the extrema scan
+        (identical results for any count).  keep_gauss=False frees the
+        Gaussian pyramid once the DoG is formed (large images)."""
         img = np.ascontiguousarray(img, dtype=np.float32)
         H, W = img.shape
         self.W, self.H, self.p = W, H, p
@@ -106,25 +112,44 @@ class OracleRun:
         self.dims = octave_dims(W, H, O)
         P = sum(h * w for h, w in self.dims)
         L = lib()
-        self.gauss_flat = np.zeros(P * (S + 3))
-        L.oracle_scale_space(_ptr(img, ctypes.c_float), W, H, ctypes.byref(p), mode,
-                             _ptr(self.gauss_flat, ctypes.c_double))
-        self.dog_flat = np.zeros(P * (S + 2))
-        L.oracle_dog(ctypes.byref(p), W, H, _ptr(self.gauss_flat, ctypes.c_double),
-                     _ptr(self.dog_flat, ctypes.c_double))
-        self.gauss = split_pyramid(self.gauss_flat, self.dims, S + 3)
-        self.dog = split_pyramid(self.dog_flat, self.dims, S + 2)
-        low = ctypes.c_long(0)
-        n = L.oracle_find_extrema(ctypes.byref(p), W, H, _ptr(self.dog_flat, ctypes.c_double),
-                                  None, None, 0, ctypes.byref(low))
-        self.cand_rec = np.zeros((max(n, 1), 4), dtype=np.int32)
-        self.cand_val = np.zeros(max(n, 1))
-        L.oracle_find_extrema(ctypes.byref(p), W, H, _ptr(self.dog_flat, ctypes.c_double),
-                              _ptr(self.cand_rec, ctypes.c_int32), _ptr(self.cand_val, ctypes.c_double),
-                              n, ctypes.byref(low))
+        set_threads(threads)
+        try:
+            gauss_flat = np.zeros(P * (S + 3))
+            L.oracle_scale_space(_ptr(img, ctypes.c_float), W, H, ctypes.byref(p), mode,
+                                 _ptr(gauss_flat, ctypes.c_double))
+            self.dog_flat = np.zeros(P * (S + 2))
+            L.oracle_dog(ctypes.byref(p), W, H, _ptr(gauss_flat, ctypes.c_double),
+                         _ptr(self.dog_flat, ctypes.c_double))
+            if keep_gauss:
+                self.gauss_flat = gauss_flat
+                self.gauss = split_pyramid(self.gauss_flat, self.dims, S + 3)
+            del gauss_flat
+            self.dog = split_pyramid(self.dog_flat, self.dims, S + 2)
+            low = ctypes.c_long(0)
+            dogp = _ptr(self.dog_flat, ctypes.c_double)
+            n = L.oracle_find_extrema_ex(ctypes.byref(p), W, H, dogp, None, None, 0, None, None, 0,
+                                         ctypes.byref(low))
+            nl = int(low.value)
+            self.cand_rec = np.zeros((max(n, 1), 4), dtype=np.int32)
+            self.cand_val = np.zeros(max(n, 1))
+            self.low_rec = np.zeros((max(nl, 1), 4), dtype=np.int32)
+            self.low_val = np.zeros(max(nl, 1))
+            L.oracle_find_extrema_ex(ctypes.byref(p), W, H, dogp, _ptr(self.cand_rec, ctypes.c_int32),
+                                     _ptr(self.cand_val, ctypes.c_double), n, _ptr(self.low_rec, ctypes.c_int32),
+                                     _ptr(self.low_val, ctypes.c_double), nl, ctypes.byref(low))
+        finally:
+            set_threads(1)
         self.cand_rec, self.cand_val = self.cand_rec[:n], self.cand_val[:n]
-        self.n_low = int(low.value)
+        self.low_rec, self.low_val = self.low_rec[:nl], self.low_val[:nl]
+        self.n_low = nl
         self.refined, self.n_singular = self.refine(self.cand_rec, self.cand_val)
+
+    def low_contrast(self):
+        """(N,5) [octave, scale, x, y, value] of the low-contrast extrema, reference order."""
+        c = np.zeros((self.low_rec.shape[0], 5))
+        c[:, :4] = self.low_rec
+        c[:, 4] = self.low_val
+        return c
 
     def refine(self, rec, val):
         rec = np.ascontiguousarray(rec, dtype=np.int32)

@@ -267,8 +267,72 @@ static double contrast_threshold(int S) {
   return ((pow(2.0, 1.0 / S) - 1) / (pow(2.0, 1.0 / 3) - 1)) * 0.015;
 }
 
-long oracle_find_extrema(const oracle_params *p, int W, int H, const double *dog, int32_t *rec,
-                         double *val, long cap, long *n_low) {
+/* One extremum list being filled: records past cap are counted, not written. */
+typedef struct {
+  int32_t *rec;
+  double *val;
+  long cap;
+} xlist;
+
+static inline void xlist_put(const xlist *L, long i, int o, int s, int x, int y, double v) {
+  if (!L->rec || i >= L->cap) return;
+  L->rec[4 * i] = o; L->rec[4 * i + 1] = s; L->rec[4 * i + 2] = x; L->rec[4 * i + 3] = y;
+  L->val[i] = v;
+}
+
+/* sift.js:212-316 on one row y of the DoG trio A, B, C: strict 26-neighbour
+ * min/max, |v| >= 0.8*thr -> candidate list, else low-contrast list (:293-306),
+ * x ascending.  nc / nl: running indices of the two lists. */
+static void scan_row(const double *A, const double *B, const double *C, int w, int y, double pix_thr, int o,
+                     int s, const xlist *cand, const xlist *lowl, long *nc, long *nl) {
+  for (int x = 1; x < w - 1; x++) {
+    const double c = B[(long)y * w + x];
+    int is_min = 1, is_max = 1;
+    for (int pl = 0; pl < 3; pl++) {
+      const double *Q = pl == 0 ? A : (pl == 1 ? B : C);
+      for (int dy = -1; dy <= 1; dy++)
+        for (int dx = -1; dx <= 1; dx++) {
+          if (pl == 1 && dy == 0 && dx == 0) continue;
+          const double v = Q[(long)(y + dy) * w + x + dx];
+          if (!(v > c)) is_min = 0;
+          if (!(v < c)) is_max = 0;
+        }
+    }
+    if (is_min || is_max) {
+      if (fabs(c) >= pix_thr) xlist_put(cand, (*nc)++, o, s, x, y, c);
+      else xlist_put(lowl, (*nl)++, o, s, x, y, c);
+    }
+  }
+}
+
+typedef struct {
+  const double *A, *B, *C;
+  int w, o, s;
+  double pix_thr;
+  long *row_nc, *row_nl;      /* per row (index y-1): counts (pass 1) / first index (pass 2) */
+  const xlist *cand, *lowl;
+  int write;
+} xscan_ctx;
+
+/* Rows 1 + [r0, r1) of one trio: pass 1 counts per row, pass 2 writes every
+ * row at its precomputed offset -- the list order is the sequential one. */
+static void xscan_rows(const void *vc, int r0, int r1) {
+  const xscan_ctx *c = (const xscan_ctx *)vc;
+  static const xlist none = {NULL, NULL, 0};
+  for (int r = r0; r < r1; r++) {
+    long nc = c->write ? c->row_nc[r] : 0, nl = c->write ? c->row_nl[r] : 0;
+    scan_row(c->A, c->B, c->C, c->w, r + 1, c->pix_thr, c->o, c->s, c->write ? c->cand : &none,
+             c->write ? c->lowl : &none, &nc, &nl);
+    if (!c->write) {
+      c->row_nc[r] = nc;
+      c->row_nl[r] = nl;
+    }
+  }
+}
+
+long oracle_find_extrema_ex(const oracle_params *p, int W, int H, const double *dog, int32_t *rec,
+                            double *val, long cap, int32_t *low_rec, double *low_val, long low_cap,
+                            long *n_low) {
   /* background.js:359-450 (scales 1..S), sift.js:212-316 */
   const int O = p->num_octaves, S = p->scales_per_octave;
   int *dims = (int *)malloc(sizeof(int) * 2 * O);
@@ -281,38 +345,37 @@ long oracle_find_extrema(const oracle_params *p, int W, int H, const double *dog
     const size_t P = (size_t)h * w;
     for (int s = 1; s < S + 1; s++) {
       const double *A = d + (size_t)(s - 1) * P, *B = d + (size_t)s * P, *C = d + (size_t)(s + 1) * P;
-      for (int y = 1; y < h - 1; y++)
-        for (int x = 1; x < w - 1; x++) {
-          const double c = B[(long)y * w + x];
-          int is_min = 1, is_max = 1;
-          for (int pl = 0; pl < 3; pl++) {
-            const double *Q = pl == 0 ? A : (pl == 1 ? B : C);
-            for (int dy = -1; dy <= 1; dy++)
-              for (int dx = -1; dx <= 1; dx++) {
-                if (pl == 1 && dy == 0 && dx == 0) continue;
-                const double v = Q[(long)(y + dy) * w + x + dx];
-                if (!(v > c)) is_min = 0;
-                if (!(v < c)) is_max = 0;
-              }
-          }
-          if (is_min || is_max) {
-            if (fabs(c) >= pix_thr) {
-              if (n < cap) {
-                rec[4 * n] = o; rec[4 * n + 1] = s; rec[4 * n + 2] = x; rec[4 * n + 3] = y;
-                val[n] = c;
-              }
-              n++;
-            } else {
-              low++;
-            }
-          }
-        }
+      const xlist cand = {rec, val, cap}, lowl = {low_rec, low_val, low_cap};
+      if (g_threads <= 1 || h < 4) {
+        for (int y = 1; y < h - 1; y++) scan_row(A, B, C, w, y, pix_thr, o, s, &cand, &lowl, &n, &low);
+        continue;
+      }
+      const int nr = h - 2;
+      long *rnc = (long *)calloc((size_t)nr, sizeof(long)), *rnl = (long *)calloc((size_t)nr, sizeof(long));
+      xscan_ctx c = {A, B, C, w, o, s, pix_thr, rnc, rnl, &cand, &lowl, 0};
+      for_rows(xscan_rows, &c, nr);
+      for (int r = 0; r < nr; r++) {  /* counts -> first index of every row */
+        const long a = rnc[r], b = rnl[r];
+        rnc[r] = n;
+        rnl[r] = low;
+        n += a;
+        low += b;
+      }
+      c.write = 1;
+      for_rows(xscan_rows, &c, nr);
+      free(rnc);
+      free(rnl);
     }
     d += (size_t)(S + 2) * P;
   }
   free(dims);
   if (n_low) *n_low = low;
   return n;
+}
+
+long oracle_find_extrema(const oracle_params *p, int W, int H, const double *dog, int32_t *rec,
+                         double *val, long cap, long *n_low) {
+  return oracle_find_extrema_ex(p, W, H, dog, rec, val, cap, NULL, NULL, 0, n_low);
 }
 
 long oracle_refine(const oracle_params *p, int W, int H, const double *dog, const int32_t *rec,

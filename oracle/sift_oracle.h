@@ -50,6 +50,14 @@ void oracle_dog(const oracle_params *p, int W, int H, const double *gauss, doubl
 long oracle_find_extrema(const oracle_params *p, int W, int H, const double *dog,
                          int32_t *rec, double *val, long cap, long *n_low);
 
+/* Same, also listing the low-contrast extrema (reference order, the
+ * reference's lowContrastKeypoints, sift.js:293-306) into low_rec / low_val
+ * (up to low_cap; NULL = count only).  With oracle_set_threads(n > 1) the rows
+ * are scanned in parallel; the lists are identical. */
+long oracle_find_extrema_ex(const oracle_params *p, int W, int H, const double *dog,
+                            int32_t *rec, double *val, long cap, int32_t *low_rec,
+                            double *low_val, long low_cap, long *n_low);
+
 /* Quadratic refinement.  out[8*i] = {octave, scaleLevel, localX, localY,
  * absoluteSigma, absoluteX, absoluteY, interpolatedValue}.  Candidates must
  * be in reference order.  *n_singular counts candidates whose Hessian had

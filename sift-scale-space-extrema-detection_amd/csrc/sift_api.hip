@@ -101,7 +101,9 @@ struct sift_ctx {
   unsigned* h_counters = nullptr;              // pinned mirror of counters
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
+  hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
   sift_timings tm{};
+  std::vector<double> oct_ms;      // per-octave Gaussian+DoG launch time of the last build
 };
 
 #define HIPCHK(call)                                                                        \
@@ -195,6 +197,7 @@ static int ctx_create(int device, sift_ctx* share, sift_ctx** out) {
     return SIFT_E_HIP;
   }
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  for (auto& e : ctx->ev_go) (void)hipEventCreate(&e);
   (void)hipEventCreateWithFlags(&ctx->ev_heavy, hipEventDisableTiming);
   // Measured on MI355X at 4K: overlapping the memory-bound scans with the
   // small octaves' Gaussians slows both (shared L2/fabric), so the overlap
@@ -243,6 +246,8 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->ev_go)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_heavy) (void)hipEventDestroy(ctx->ev_heavy);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
@@ -457,6 +462,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     }
     HIPCHK(launch_gauss_dog(P, L, ls));
     if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ls));
+    HIPCHK(hipEventRecord(ctx->ev_go[o], ls));
     if (ls != ctx->stream) {
       HIPCHK(hipEventRecord(ctx->ev_hi_join, ls));
       HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_hi_join, 0));
@@ -482,6 +488,20 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   return SIFT_OK;
 }
 
+// Gaussian+DoG timings of the last build (its events must have completed):
+// the whole pass, octave 0's launch and every octave's launch.
+static void read_gauss_times(sift_ctx* ctx) {
+  float b = 0;
+  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]) == hipSuccess) ctx->tm.gauss_dog_ms = b;
+  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
+  ctx->oct_ms.assign(ctx->P.O, 0.0);
+  hipEvent_t prev = ctx->ev[1];
+  for (int o = ctx->o_first; o < ctx->P.O; ++o) {
+    if (hipEventElapsedTime(&b, prev, ctx->ev_go[o]) == hipSuccess) ctx->oct_ms[o] = b;
+    prev = ctx->ev_go[o];
+  }
+}
+
 extern "C" {
 
 int sift_build_scale_space(sift_ctx* ctx, const float* img, int width, int height, size_t stride_px,
@@ -489,12 +509,10 @@ int sift_build_scale_space(sift_ctx* ctx, const float* img, int width, int heigh
   int rc = build_common(ctx, img, nullptr, width, height, stride_px, p, sig);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  float a = 0, b = 0;
+  float a = 0;
   (void)hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
-  (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
   ctx->tm.h2d_ms = a;
-  ctx->tm.gauss_dog_ms = b;
-  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
+  read_gauss_times(ctx);
   return SIFT_OK;
 }
 
@@ -503,11 +521,8 @@ int sift_build_scale_space_device(sift_ctx* ctx, const float* d_img, int width, 
   int rc = build_common(ctx, nullptr, d_img, width, height, stride_px, p, sig);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(ctx->stream));
-  float b = 0;
-  (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
   ctx->tm.h2d_ms = 0;
-  ctx->tm.gauss_dog_ms = b;
-  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
+  read_gauss_times(ctx);
   return SIFT_OK;
 }
 
@@ -858,8 +873,9 @@ static int refine_settle(sift_ctx* ctx) {
   ctx->n_sing = h[kCntSing];
   if (std::getenv("SIFT_DEBUG_REFINE"))
     std::fprintf(stderr,
-                 "refine uncertain %u: det %u alpha %u omega %u edge_dt %u edge_int %u round %u | iter %u %u %u %u %u\n",
-                 h[kCntUnc], h[16], h[17], h[18], h[19], h[20], h[21], h[22], h[23], h[24], h[25], h[26]);
+                 "refine uncertain %u: det %u alpha %u omega %u edge_dt %u edge_int %u round %u | iter %u %u %u %u %u"
+                 " | output precision %u\n",
+                 h[kCntUnc], h[16], h[17], h[18], h[19], h[20], h[21], h[22], h[23], h[24], h[25], h[26], h[27]);
   return SIFT_OK;
 }
 
@@ -1047,12 +1063,11 @@ static int detect_finish(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* 
     rc = run_refine(ctx);
   }
   if (rc) return rc;
-  float a = 0, b = 0;
+  float a = 0;
   (void)hipEventSynchronize(ctx->ev[6]);
   if (ctx->detect_host_img && hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->tm.h2d_ms = a;
   if (!ctx->detect_host_img) ctx->tm.h2d_ms = 0;
-  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]) == hipSuccess) ctx->tm.gauss_dog_ms = b;
-  if (hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[7]) == hipSuccess) ctx->tm.gauss_oct0_ms = b;
+  read_gauss_times(ctx);
   read_stage_times(ctx, true, true);
   rc = sift_copy_keypoints(ctx, out, cap, n_out);
   if (rc) return rc;
@@ -1122,6 +1137,16 @@ int sift_last_counts(sift_ctx* ctx, size_t* nc, size_t* nl, size_t* nk, size_t* 
 int sift_last_timings(sift_ctx* ctx, sift_timings* t) {
   if (!ctx || !t) return SIFT_E_ARG;
   *t = ctx->tm;
+  return SIFT_OK;
+}
+
+int sift_last_octave_timings(sift_ctx* ctx, double* ms, int cap, int* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  const int n = (int)ctx->oct_ms.size();
+  if (n_out) *n_out = n;
+  if (!ms) return SIFT_OK;
+  if (cap < n) return set_err(ctx, SIFT_E_CAPACITY, "destination too small (one per octave)");
+  for (int o = 0; o < n; ++o) ms[o] = ctx->oct_ms[o];
   return SIFT_OK;
 }
 

@@ -376,8 +376,16 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
   if (4.0 * np * (double)P.oct[0].h * P.oct[0].w >= 4294967296.0) return hipErrorInvalidValue;
   // SIFT_XLDS (bytes, experiments): unused dynamic LDS per block, capping the
   // scan's blocks per CU (160 KiB / SIFT_XLDS) to leave CUs to other images.
-  static const int xlds = [] { const char* e = std::getenv("SIFT_XLDS"); return e ? std::atoi(e) : 0; }();
-  if (xlds > 65536) (void)hipFuncSetAttribute((const void*)k_extrema, hipFuncAttributeMaxDynamicSharedMemorySize, xlds);
+  // Values outside [0, 160 KiB] are ignored.
+  static const int xlds = [] {
+    const char* e = std::getenv("SIFT_XLDS");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return (v > 0 && v <= 160 * 1024) ? (int)v : 0;
+  }();
+  if (xlds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_extrema, hipFuncAttributeMaxDynamicSharedMemorySize, xlds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_extrema, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), xlds, st, P, L);
   return hipGetLastError();
 }

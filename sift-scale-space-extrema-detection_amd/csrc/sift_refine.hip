@@ -37,11 +37,20 @@ __device__ __forceinline__ double round_margin(double v) {
 struct StepOut {
   int state;         // 0 continue (moved), 1 keep, 2 discard, 3 singular
   bool uncertain;
-  unsigned why;      // diagnostic: which decisions were uncertain (bits 0..5)
+  unsigned why;      // diagnostic: which decisions were uncertain (bits 0..6)
   double a[3];
   double omega;
+  double ea, eo;     // error bounds of alpha (each entry) and omega (0 on exact planes)
   int s, m, n;       // position after the step (moved) or of the keypoint
 };
+
+// Largest error of a kept keypoint's absolute (x, y, sigma) that the fast
+// pass may leave (the parity bar is 1e-4; the bounds below are first-order
+// with a factor kSafe of slack).  The absolute coordinates scale the offset
+// alpha by 2^(o-1) -- 16 at octave 5 of an 8K pyramid, where the DoG values
+// are small and fp32 rounding of the planes moves alpha by ~1e-5 -- so a
+// keypoint whose bound exceeds this is recomputed from exact fp64 patches.
+constexpr double kKeypointTol = 1e-5;
 
 // One iteration of background.js:480-664 on the patch d[k][a][c]
 // (k: scale s-1+k, a: row m-1+a, c: col n-1+c).  `delta` bounds the error of
@@ -66,6 +75,8 @@ __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int 
   StepOut R;
   R.uncertain = false;
   R.why = 0;
+  R.ea = 0.0;
+  R.eo = 0.0;
   const double cc = DP(1, 1, 1);
   const double g0 = (DP(2, 1, 1) - DP(0, 1, 1)) / 2;
   const double g1 = (DP(1, 2, 1) - DP(1, 0, 1)) / 2;
@@ -147,8 +158,10 @@ __device__ inline StepOut refine_step(const double* d, int o, int s, int m, int 
     const double omega = value + (((0.5 * R.a[0]) * g0) + ((0.5 * R.a[1]) * g1) + ((0.5 * R.a[2]) * g2));
     R.omega = omega;
     R.s = s; R.m = m; R.n = n;
+    R.ea = Ea;
     if (delta > 0 || dval > 0) {
       const double Eo = kSafe * (dval + 0.5 * (Ea * (fabs(g0) + fabs(g1) + fabs(g2)) + (a1 + 3 * Ea) * dG)) + 1e-300;
+      R.eo = Eo;
       if (fabs(fabs(omega) - thr) <= Eo) R.uncertain = true, R.why |= 4;
     }
     if (fabs(omega) < thr) { R.state = 2; return R; }
@@ -285,8 +298,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       if (R.state == 3) { status = kRefSingular; break; }
       if (R.state == 2) { status = kRefDiscard; break; }
       if (R.state == 1) {
+        Keypoint& k = L.kp[i];
+        make_keypoint(k, o, R, P.S, L.min_blur, L.min_interpixel_distance, (P.row0 * 2) >> o);
+        if (!EXACT) {
+          // Output precision: |d abs_x|, |d abs_y| <= 2^(o-1) Ea; |d abs_sigma|
+          // <= abs_sigma (ln 2 / S) Ea; |d interp_value| <= Eo.
+          const double e_xy = ldexp(R.ea, o - 1);
+          const double e_sig = k.abs_sigma * (0.6931471805599453 / P.S) * R.ea;
+          if (e_xy > kKeypointTol || e_sig > kKeypointTol || R.eo > 1e-3 * kKeypointTol) {
+            unc = true;
+            atomicAdd(&L.counters[27], 1u);
+            break;
+          }
+        }
         status = kRefKeep;
-        make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance, (P.row0 * 2) >> o);
         break;
       }
       s = R.s; m = R.m; n = R.n;

@@ -58,7 +58,10 @@ const contexts = new Map();
 function deviceState(device = 0) {
   let st = contexts.get(device);
   if (!st) {
-    st = { ctx: native.createContext(device), gen: 0, stage: null, W: 0, H: 0, params: null };
+    // queue: detectAsync jobs of this context run one after another (a native
+    // context is not re-entrant; the addon rejects any call while a job runs).
+    st = { ctx: native.createContext(device), gen: 0, stage: null, W: 0, H: 0, params: null,
+      queue: Promise.resolve() };
     contexts.set(device, st);
   }
   return st;
@@ -144,6 +147,9 @@ function flatten(pyramid) {
 // Input (W, H) of a pyramid: octave 0 is the 2x upsample (background.js:84).
 function inputDimsOf(pyramid) {
   const [h0, w0] = planeDims(pyramid[0][0].image);
+  if (h0 % 2 || w0 % 2 || h0 < 2 || w0 < 2) {
+    throw new RangeError('octave 0 of a pyramid is the 2x upsample of the input (background.js:84): even dims expected');
+  }
   return [w0 / 2, h0 / 2];
 }
 
@@ -367,16 +373,28 @@ export function detect(input_image, { number_of_octaves = 5, scales_per_octave =
   return keypointsFromNative(r);
 }
 
-export async function detectAsync(input_image, opts = {}) {
+// Calls on one device are serialised: each job starts when the previous one
+// on that device has settled (Promise.all over many images is fine); a
+// synchronous call on the device while a job runs throws (SIFT_E_BUSY).
+export function detectAsync(input_image, opts = {}) {
   const { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8, assumed_blur = 0.5,
     min_interpixel_distance = 0.5, device = 0 } = opts;
-  let img = toGray(input_image);
   const st = deviceState(device);
-  if (img.rgba) img = { width: img.width, height: img.height, data: native.rgbaToGray(st.ctx, img.data, img.width, img.height, false).gray };
-  const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
-  bump(st, 'detecting', img.width, img.height, params);
-  const r = await native.detectAsync(st.ctx, img.data, img.width, img.height, params);
-  return keypointsFromNative(r);
+  const run = async () => {
+    let img = toGray(input_image);
+    if (img.rgba) img = { width: img.width, height: img.height, data: native.rgbaToGray(st.ctx, img.data, img.width, img.height, false).gray };
+    const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
+    bump(st, 'detecting', img.width, img.height, params);
+    const r = await native.detectAsync(st.ctx, img.data, img.width, img.height, params);
+    return keypointsFromNative(r);
+  };
+  // An idle device starts the job at once (the native job is queued before
+  // this returns); otherwise it waits for the jobs ahead of it.
+  st.pending = (st.pending || 0) + 1;
+  const job = st.pending === 1 ? run() : st.queue.then(run, run);
+  const done = () => { st.pending -= 1; };
+  st.queue = job.then(done, done);
+  return job;
 }
 
 export function lastCounts(device = 0) {

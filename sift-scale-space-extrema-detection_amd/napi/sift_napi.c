@@ -38,19 +38,40 @@ static napi_value throw_sift(napi_env env, struct sift_ctx *ctx, int rc, const c
   return NULL;
 }
 
+/* The JS handle of a context.  A sift_ctx is not re-entrant (include/sift_hip.h):
+ * while a detectAsync job runs on the libuv pool the context is `busy` and
+ * every other call on it is rejected instead of racing the worker thread. */
+typedef struct {
+  struct sift_ctx *ctx;
+  int busy;
+} ctx_box;
+
 static void ctx_finalize(napi_env env, void *data, void *hint) {
   (void)env;
   (void)hint;
-  if (data) sift_ctx_destroy((struct sift_ctx *)data);
+  ctx_box *b = (ctx_box *)data;
+  if (!b) return;
+  if (b->ctx) sift_ctx_destroy(b->ctx);
+  free(b);
 }
 
-static struct sift_ctx *get_ctx(napi_env env, napi_value v) {
+static ctx_box *get_box(napi_env env, napi_value v) {
   void *p = NULL;
   if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
     napi_throw_type_error(env, NULL, "expected a sift context");
     return NULL;
   }
-  return (struct sift_ctx *)p;
+  ctx_box *b = (ctx_box *)p;
+  if (b->busy) {
+    napi_throw_error(env, "SIFT_E_BUSY", "sift context busy: a detectAsync job is still running on it");
+    return NULL;
+  }
+  return b;
+}
+
+static struct sift_ctx *get_ctx(napi_env env, napi_value v) {
+  ctx_box *b = get_box(env, v);
+  return b ? b->ctx : NULL;
 }
 
 static int get_i32_prop(napi_env env, napi_value obj, const char *name, int def) {
@@ -123,8 +144,19 @@ static napi_value js_create_context(napi_env env, napi_callback_info info) {
   struct sift_ctx *ctx = NULL;
   int rc = sift_ctx_create(dev, &ctx);
   if (rc) return throw_sift(env, NULL, rc, "sift_ctx_create (is a HIP device visible?)");
+  ctx_box *b = (ctx_box *)calloc(1, sizeof(ctx_box));
+  if (!b) {
+    sift_ctx_destroy(ctx);
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  b->ctx = ctx;
   napi_value ext;
-  NAPI_CALL(env, napi_create_external(env, ctx, ctx_finalize, NULL, &ext));
+  if (napi_create_external(env, b, ctx_finalize, NULL, &ext) != napi_ok) {
+    ctx_finalize(env, b, NULL);
+    napi_throw_error(env, NULL, "napi_create_external failed");
+    return NULL;
+  }
   return ext;
 }
 
@@ -220,7 +252,8 @@ static napi_value load_common(napi_env env, napi_callback_info info, int which) 
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   struct sift_ctx *ctx = get_ctx(env, argv[0]);
   if (!ctx) return NULL;
-  const float *flat = (const float *)typed_data(env, argv[1], napi_float32_array, NULL);
+  size_t len = 0;
+  const float *flat = (const float *)typed_data(env, argv[1], napi_float32_array, &len);
   if (!flat) {
     napi_throw_type_error(env, NULL, "planes must be a Float32Array");
     return NULL;
@@ -230,6 +263,26 @@ static napi_value load_common(napi_env env, napi_callback_info info, int which) 
   napi_get_value_int32(env, argv[3], &h);
   sift_params p;
   read_params(env, argv[4], &p);
+  /* The C entry points copy sum_o rows_o*cols_o*(S+2) (or S+3) floats: the
+   * array must hold exactly that many, or the copy would read past its end. */
+  if (w < 1 || h < 1 || p.num_octaves < 1 || p.num_octaves > 64 || p.scales_per_octave < 1) {
+    napi_throw_range_error(env, NULL, "bad pyramid geometry");
+    return NULL;
+  }
+  int32_t dims[128];
+  if (sift_octave_dims(w, h, p.num_octaves, dims) != SIFT_OK) {
+    napi_throw_range_error(env, NULL, "bad pyramid geometry");
+    return NULL;
+  }
+  size_t px = 0;
+  for (int o = 0; o < p.num_octaves; ++o) px += (size_t)dims[2 * o] * (size_t)dims[2 * o + 1];
+  const size_t want = px * (size_t)(p.scales_per_octave + (which ? 3 : 2));
+  if (len != want) {
+    char buf[160];
+    snprintf(buf, sizeof buf, "pyramid holds %zu values, the geometry needs %zu", len, want);
+    napi_throw_range_error(env, NULL, buf);
+    return NULL;
+  }
   int rc = which ? sift_load_scale_space(ctx, flat, w, h, &p) : sift_load_dog(ctx, flat, w, h, &p);
   if (rc) return throw_sift(env, ctx, rc, which ? "sift_load_scale_space" : "sift_load_dog");
   return NULL;
@@ -393,6 +446,7 @@ typedef struct {
   napi_deferred deferred;
   napi_ref img_ref;
   napi_ref ctx_ref;
+  ctx_box *box;
   struct sift_ctx *ctx;
   const float *img;
   int w, h, rc;
@@ -408,6 +462,7 @@ static void detect_execute(napi_env env, void *data) {
 
 static void detect_complete(napi_env env, napi_status status, void *data) {
   detect_job *j = (detect_job *)data;
+  j->box->busy = 0;
   if (status == napi_ok && (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR)) {
     size_t sing = 0;
     sift_last_counts(j->ctx, NULL, NULL, NULL, &sing, NULL);
@@ -437,8 +492,9 @@ static napi_value js_detect_async(napi_env env, napi_callback_info info) {
   size_t argc = 5;
   napi_value argv[5];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  struct sift_ctx *ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
+  ctx_box *box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  struct sift_ctx *ctx = box->ctx;
   size_t len = 0;
   const float *img = (const float *)typed_data(env, argv[1], napi_float32_array, &len);
   int32_t w = 0, h = 0;
@@ -449,6 +505,7 @@ static napi_value js_detect_async(napi_env env, napi_callback_info info) {
     return NULL;
   }
   detect_job *j = (detect_job *)calloc(1, sizeof(detect_job));
+  j->box = box;
   j->ctx = ctx;
   j->img = img;
   j->w = w;
@@ -461,6 +518,7 @@ static napi_value js_detect_async(napi_env env, napi_callback_info info) {
   napi_create_string_utf8(env, "sift_detect", NAPI_AUTO_LENGTH, &name);
   NAPI_CALL(env, napi_create_async_work(env, NULL, name, detect_execute, detect_complete, j, &j->work));
   NAPI_CALL(env, napi_queue_async_work(env, j->work));
+  box->busy = 1;  /* until detect_complete (JS thread) */
   return promise;
 }
 

@@ -52,7 +52,7 @@ ABI_SYMBOLS = (
     "sift_keypoint_origins", "sift_set_row_origin", "sift_order_after",
     "sift_rgba_to_gray", "sift_rgba_to_gray_device", "sift_build_scale_space_rgba", "sift_detect_rgba",
     "sift_plane_image", "sift_plane_image_device", "sift_detect_begin_async", "sift_detect_end_async",
-    "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device",
+    "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device", "sift_last_octave_timings",
 )
 
 
@@ -151,6 +151,7 @@ def lib():
         "sift_ctx_create_shared": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
         "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
         "sift_last_timings": (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
+        "sift_last_octave_timings": (ctypes.c_int, [vp, dp, ctypes.c_int, ip]),
         "sift_device_keypoints": (ctypes.c_int, [vp, ctypes.POINTER(vp), szp]),
         "sift_stream": (vp, [vp]),
         "sift_synchronize": (ctypes.c_int, [vp]),
@@ -528,6 +529,15 @@ class Context:
         self._check(self._L.sift_last_timings(self._h, ctypes.byref(t)), "sift_last_timings")
         return dict(gauss_dog_ms=t.gauss_dog_ms, extrema_ms=t.extrema_ms, refine_ms=t.refine_ms,
                     h2d_ms=t.h2d_ms, gauss_oct0_ms=t.gauss_oct0_ms)
+
+    def octave_timings(self):
+        """Per-octave Gaussian+DoG launch ms of the last build / detection."""
+        n = ctypes.c_int()
+        self._check(self._L.sift_last_octave_timings(self._h, None, 0, ctypes.byref(n)), "sift_last_octave_timings")
+        out = np.zeros(max(n.value, 1))
+        self._check(self._L.sift_last_octave_timings(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                                     out.shape[0], ctypes.byref(n)), "sift_last_octave_timings")
+        return [float(v) for v in out[:n.value]]
 
     def stream(self):
         return self._L.sift_stream(self._h)

@@ -279,12 +279,25 @@ def _device_lists(ctx, n, torch, dev):
     return kp[:n], org[:n]
 
 
+def torch_ready(t):
+    """Wait until torch's work producing `t` is done.  The C ABI runs on its
+    own HIP stream (another runtime instance than torch's), which nothing
+    orders after torch's stream: every sift_* call that reads a buffer torch
+    wrote (the image, a gathered base) must come after this."""
+    if t.is_cuda:
+        import torch
+        torch.cuda.current_stream(t.device).synchronize()
+
+
 def run_shard_device(ctx, d_img, params, plan, r):
     """Shard r from the whole image `d_img` (H x W fp32 torch tensor on ctx's
     device): (keypoints uint8 [n, 48], origins int32 [n, 4], owned base rows
-    fp64 [rows, cols] or None), all on the device."""
+    fp64 [rows, cols] or None), all on the device.  The sift_* copies into
+    the returned tensors complete before they return, so torch may read them
+    at once."""
     import torch
     dev = d_img.device
+    torch_ready(d_img)
     lo, hi = plan.bands[r]
     c0, c1 = plan.crops[r]
     K = plan.K
@@ -323,6 +336,8 @@ def run_tail_device(ctx, d_base, params, plan):
     h, w = octave_dims(plan.width, plan.height, plan.num_octaves)[plan.K + 1]
     if tuple(d_base.shape) != (h, w):
         raise ValueError("gathered base %s != octave %d dims %s" % (tuple(d_base.shape), plan.K + 1, (h, w)))
+    d_base = d_base.contiguous()
+    torch_ready(d_base)  # the all-gather / concatenation that made it is only enqueued on torch's stream
     n = ctx.detect_from_seed_device(d_base.data_ptr(), plan.K + 1, plan.width, plan.height, p)
     return _device_lists(ctx, n, torch, d_base.device)
 

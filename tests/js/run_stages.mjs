@@ -62,8 +62,15 @@ if (mode !== 'schedule-only') {
     minBlurLevel: P.min_blur, minInterpixelDistance: P.min_interpixel_distance } });
   out.worker = { types: posted.map(m => m.type), matrix2dRows: ss[0][0].image.length,
     refined: posted[posted.length - 1].refinedKeypoints.length };
-  sift.detectAsync(image, { number_of_octaves: P.num_octaves, scales_per_octave: P.scales_per_octave }).then(k => {
-    out.detectAsync = k.length;
+  // two overlapping async jobs on one device run one after the other; a
+  // synchronous call while one runs is rejected, not raced
+  const aopts = { number_of_octaves: P.num_octaves, scales_per_octave: P.scales_per_octave,
+    min_blur_level: P.min_blur, assumed_blur: P.assumed_blur };
+  const jobs = [sift.detectAsync(image, aopts), sift.detectAsync(image, aopts)];
+  try { sift.lastCounts(); out.busyCode = null; } catch (e) { out.busyCode = e.code || String(e); }
+  Promise.all(jobs).then(ks => {
+    out.detectAsync = ks.map(k => k.length);
+    out.countsAfter = sift.lastCounts().keypoints;
     fs.writeFileSync(outPath, JSON.stringify(out));
   });
 } else {

@@ -18,37 +18,10 @@ import pytest
 import oracle as orc
 import sift_amd
 from golden_util import Golden, case_names
+from parity_util import check_candidates, check_keypoints, oracle_params as _oracle_params
 from sift_amd.synth import blob_image
 
 pytestmark = pytest.mark.gpu
-
-XY_SIGMA_TOL = 1e-4
-
-
-def params_of(g, flags=0):
-    P = g.params
-    return sift_amd.make_params(P["num_octaves"], P["scales_per_octave"], P["min_blur"], P["assumed_blur"],
-                                P["min_interpixel_distance"], flags)
-
-
-def check_candidates(c, ref, value_rtol=2 ** -23):
-    """c: EXTREMUM_DTYPE array; ref: (N,5) [o, s, x, y, value]."""
-    assert c.shape[0] == ref.shape[0], (c.shape[0], ref.shape[0])
-    got = np.stack([c["octave"], c["scale"], c["x"], c["y"]], axis=1)
-    np.testing.assert_array_equal(got, ref[:, :4].astype(np.int64))
-    np.testing.assert_allclose(c["value"], ref[:, 4], rtol=value_rtol, atol=1e-15)
-
-
-def check_keypoints(k, ref):
-    """k: KEYPOINT_DTYPE array; ref: (M,8) reference order."""
-    assert k.shape[0] == ref.shape[0], (k.shape[0], ref.shape[0])
-    ints = np.stack([k["octave"], k["scale_level"], k["local_x"], k["local_y"]], axis=1)
-    np.testing.assert_array_equal(ints, ref[:, :4].astype(np.int64))
-    np.testing.assert_allclose(k["abs_sigma"], ref[:, 4], rtol=0, atol=XY_SIGMA_TOL)
-    np.testing.assert_allclose(k["abs_x"], ref[:, 5], rtol=0, atol=XY_SIGMA_TOL)
-    np.testing.assert_allclose(k["abs_y"], ref[:, 6], rtol=0, atol=XY_SIGMA_TOL)
-    np.testing.assert_allclose(k["interp_value"], ref[:, 7], rtol=0, atol=1e-6)
-
 
 @pytest.mark.parametrize("name", case_names())
 def test_detect_matches_reference(gpu_ctx, name):
@@ -88,11 +61,6 @@ def test_stage_api_matches_reference(gpu_ctx, name):
     kp, sing = gpu_ctx.refine()
     check_keypoints(kp, g.refined)
     assert sing == 0
-
-
-def _oracle_params(p):
-    return orc.make_params(p.num_octaves, p.scales_per_octave, p.min_blur, p.assumed_blur,
-                           p.min_interpixel_distance)
 
 
 @pytest.mark.parametrize("W,H,O,S,seed", [(1920, 1080, 4, 5, 11), (640, 480, 5, 3, 12), (333, 517, 4, 4, 13)])

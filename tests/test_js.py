@@ -74,7 +74,9 @@ def test_js_stage_chain_matches_reference(name):
     np.testing.assert_allclose(k[:, 4:7], g.refined[:, 4:7], rtol=0, atol=1e-4)
     assert out["foreignCandidates"] == ref.shape[0]
     assert out["detect"] == g.refined.shape[0]
-    assert out["detectAsync"] >= 0
+    assert out["detectAsync"] == [g.refined.shape[0]] * 2  # serialised on the one context
+    assert out["busyCode"] == "SIFT_E_BUSY"
+    assert out["countsAfter"] == g.refined.shape[0]
     w = out["worker"]
     assert w["types"] == ["received-gaussian-scale-space", "received-difference-of-gaussians",
                           "received-candidate-keypoints", "received-refined-keypoints"]
