@@ -15,8 +15,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-CONV_2D = 0
-CONV_SEPARABLE = 1
+CONV_2D = 0                 # the reference's 2D kernel and summation order
+CONV_SEPARABLE = 1          # the same operator, rows then columns
+CONV_SEPARABLE_FMA_VH = 2   # columns then rows, fma chains: the HIP path's own order (bit-exact pin)
 
 
 class OracleParams(ctypes.Structure):

@@ -194,6 +194,53 @@ static void blur_sep(const double *in, double *out, int h, int w, double sig) {
   free(wt);
 }
 
+/* The GPU's operation order (k_gauss_dog, sift_exact.h): vertical pass then
+ * horizontal, each output an fma chain over the taps in increasing order,
+ * starting from 0.0.  Not the reference's order (that is CONV_2D); it pins
+ * the HIP path bit for bit: its fp64 values, hence its fp32 planes, extrema
+ * ties and low-contrast decisions, are these. */
+static void sep_rows_v_fma(const void *vc, int y0, int y1) {
+  const sep_ctx *c = (const sep_ctx *)vc;
+  const int h = c->h, w = c->w, r = c->r, n = c->n;
+  for (int y = y0; y < y1; y++)
+    for (int x = 0; x < w; x++) {
+      double acc = 0.0;
+      for (int j = 0; j < n; j++) acc = fma(c->wt[j], c->in[(long)clampi(y + j - r, 0, h - 1) * w + x], acc);
+      c->out[(long)y * w + x] = acc;
+    }
+}
+
+static void sep_rows_h_fma(const void *vc, int y0, int y1) {
+  const sep_ctx *c = (const sep_ctx *)vc;
+  const int w = c->w, r = c->r, n = c->n;
+  for (int y = y0; y < y1; y++)
+    for (int x = 0; x < w; x++) {
+      double acc = 0.0;
+      for (int i = 0; i < n; i++) acc = fma(c->wt[i], c->in[(long)y * w + clampi(x + i - r, 0, w - 1)], acc);
+      c->out[(long)y * w + x] = acc;
+    }
+}
+
+static void blur_sep_fma_vh(const double *in, double *out, int h, int w, double sig) {
+  int r = (int)js_round(3.0 * sig);
+  int n = 2 * r + 1;
+  double *wt = (double *)malloc(sizeof(double) * n);
+  double sum = 0.0;
+  for (int i = 0; i < n; i++) {
+    double a = i - r;
+    wt[i] = exp(((a * a) / (sig * sig)) * -0.5);
+    sum += wt[i];
+  }
+  for (int i = 0; i < n; i++) wt[i] /= sum;
+  double *tmp = (double *)malloc(sizeof(double) * (size_t)h * w);
+  sep_ctx cv = {in, tmp, wt, h, w, r, n};
+  for_rows(sep_rows_v_fma, &cv, h);
+  sep_ctx ch = {tmp, out, wt, h, w, r, n};
+  for_rows(sep_rows_h_fma, &ch, h);
+  free(tmp);
+  free(wt);
+}
+
 int oracle_scale_space(const float *img, int W, int H, const oracle_params *p, int mode,
                        double *gauss) {
   /* background.js:71-237 */
@@ -228,6 +275,8 @@ int oracle_scale_space(const float *img, int W, int H, const oracle_params *p, i
         memcpy(plane, base, sizeof(double) * (size_t)h * w);
       } else if (mode == ORACLE_CONV_2D) {
         blur_2d(base, plane, h, w, sigma[o * NS + s]);
+      } else if (mode == ORACLE_CONV_SEPARABLE_FMA_VH) {
+        blur_sep_fma_vh(base, plane, h, w, sigma[o * NS + s]);
       } else {
         blur_sep(base, plane, h, w, sigma[o * NS + s]);
       }

@@ -25,7 +25,11 @@ typedef struct {
   double min_interpixel_distance;
 } oracle_params;
 
-enum { ORACLE_CONV_2D = 0, ORACLE_CONV_SEPARABLE = 1 };
+/* CONV_2D: the reference's 2D kernel and summation order (sift.js:96-144).
+ * CONV_SEPARABLE: the same operator separably (rows, then columns).
+ * CONV_SEPARABLE_FMA_VH: columns then rows, fma chains -- the HIP path's own
+ * operation order (a bit-exact pin of its fp64 values, not of the reference). */
+enum { ORACLE_CONV_2D = 0, ORACLE_CONV_SEPARABLE = 1, ORACLE_CONV_SEPARABLE_FMA_VH = 2 };
 
 /* dims[2*o] = h_o, dims[2*o+1] = w_o; returns sum_o h_o*w_o. */
 long oracle_octave_dims(int W, int H, int O, int *dims);

@@ -10,21 +10,32 @@
 
 namespace sift {
 
-// LDS doubles one wave needs: 3 rows x (2R+3) vertical sums + 4 scales x 9 outputs.
-__host__ __device__ inline int exact_scratch_doubles(int rmax) { return 3 * (2 * rmax + 3) + 36; }
+// LDS doubles one wave needs: 4 L-scales x 3 rows x (2R+3) vertical sums.
+__host__ __device__ inline int exact_scratch_doubles(int rmax) { return 12 * (2 * rmax + 3) + 36; }
 
-// L at rows y-1..y+1, cols x-1..x+1 of L-scale t -> out[9] (row-major).
-// Requires blockDim.x == 64 (one wave): __syncthreads() is a wave barrier.
-__device__ inline void wave_L_patch(const Pyramid& P, int o, int t, int y, int x, double* sh,
-                                    double* out) {
+// DoG patch d[k][a][c] for DoG scales s-1+k (k = 0..2), rows y-1+a, cols
+// x-1+c, from the L-scales s-1..s+2.  Result in lds d27[27] (visible to all
+// lanes).  Requires blockDim.x == 64 (one wave): __syncthreads() is a wave
+// barrier.  The four L-scales' vertical sums run side by side (one pass over
+// 12 (2r+3) independent fma chains), then 36 lanes form the horizontal sums:
+//   V_t[a][c] = sum_j w_j B(clamp(y-1+a-r+j), clamp(x-1-r+c))
+//   L_t[a][b] = sum_i w_i V_t[a][b + i]            (output column x-1+b)
+__device__ inline void wave_dog_patch(const Pyramid& P, int o, int s, int y, int x, double* sh,
+                                      double* Lbuf /*36*/, double* d27) {
   const Octave& oc = P.oct[o];
-  const int h = oc.h, w = oc.w, r = oc.rad[t];
-  const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
+  const int h = oc.h, w = oc.w;
   const int lane = threadIdx.x & 63;
-  const int nc = 2 * r + 3;  // columns x-1-r .. x+1+r
-  // vertical: V[a][c] = sum_j w_j B(clamp(y-1+a-r+j), clamp(x-1-r+c))
-  for (int idx = lane; idx < 3 * nc; idx += 64) {
-    const int a = idx / nc, c = idx - nc * a;
+  const int nc0 = 2 * oc.rad[s - 1] + 3, nc1 = 2 * oc.rad[s] + 3, nc2 = 2 * oc.rad[s + 1] + 3,
+            nc3 = 2 * oc.rad[s + 2] + 3;
+  const int o1 = 3 * nc0, o2 = o1 + 3 * nc1, o3 = o2 + 3 * nc2, o4 = o3 + 3 * nc3;
+  for (int idx = lane; idx < o4; idx += 64) {
+    const int k = idx >= o3 ? 3 : idx >= o2 ? 2 : idx >= o1 ? 1 : 0;
+    const int base = k == 3 ? o3 : k == 2 ? o2 : k == 1 ? o1 : 0;
+    const int nc = k == 3 ? nc3 : k == 2 ? nc2 : k == 1 ? nc1 : nc0;
+    const int t = s - 1 + k, r = oc.rad[t];
+    const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
+    const int li = idx - base;
+    const int a = li / nc, c = li - nc * a;
     const int xx = clampi(x - 1 - r + c, 0, w - 1);
     const int yb = y - 1 + a - r;
     double acc = 0.0;
@@ -32,22 +43,18 @@ __device__ inline void wave_L_patch(const Pyramid& P, int o, int t, int y, int x
     sh[idx] = acc;
   }
   __syncthreads();
-  // horizontal: L[a][b] = sum_i w_i V[a][b + i]  (output column x-1+b)
-  if (lane < 9) {
-    const int a = lane / 3, b = lane - 3 * a;
+  if (lane < 36) {
+    const int k = lane / 9, q = lane - 9 * k;
+    const int a = q / 3, b = q - 3 * a;
+    const int base = k == 3 ? o3 : k == 2 ? o2 : k == 1 ? o1 : 0;
+    const int nc = k == 3 ? nc3 : k == 2 ? nc2 : k == 1 ? nc1 : nc0;
+    const int t = s - 1 + k, r = oc.rad[t];
+    const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
     double acc = 0.0;
-    for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], sh[a * nc + b + i], acc);
-    out[lane] = acc;
+    for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], sh[base + a * nc + b + i], acc);
+    Lbuf[lane] = acc;
   }
   __syncthreads();
-}
-
-// DoG patch d[k][a][c] for DoG scales s-1+k (k = 0..2), rows y-1+a, cols
-// x-1+c: L-scales s-1..s+2.  Result in lds d27[27] (visible to all lanes).
-__device__ inline void wave_dog_patch(const Pyramid& P, int o, int s, int y, int x, double* sh,
-                                      double* Lbuf /*36*/, double* d27) {
-  for (int k = 0; k < 4; ++k) wave_L_patch(P, o, s - 1 + k, y, x, sh, Lbuf + 9 * k);
-  const int lane = threadIdx.x & 63;
   if (lane < 27) {
     const int k = lane / 9, q = lane - 9 * k;
     d27[lane] = Lbuf[9 * k + q] - Lbuf[9 * (k + 1) + q];

@@ -12,8 +12,26 @@ struct Keypoint {
   double abs_x, abs_y, abs_sigma, interp_value;
 };
 
+constexpr int kFX = 60;      // fused extrema: tile stride in x (64 computed columns, 60 owned, 60 decided)
+constexpr int kFY = 30;      // ... in y (32 computed rows, 30 owned, 30 decided)
+
+// Extrema decisions fused into the Gaussian+DoG pass of one octave (see
+// k_gauss_dog): bitmap words of kFX columns, word bx of a row = tile column
+// bx, bit b <-> x = kFX bx + 1 + b.
+struct FusedExtrema {
+  unsigned long long* bitmap;  // (scale 1, row 0, word 0) of the octave: [S][h][nw]
+  unsigned* rowcount;          // (scale 1, row 0) of the octave: [S][h]
+  int nw;                      // words per row (= tile columns of the launch)
+  unsigned* amb_keys;          // keys needing an exact fp64 decision
+  unsigned* counters;          // [0] ambiguous, [1] low-contrast
+  unsigned amb_cap;
+  float c_lo, c_hi;            // fp32 contrast thresholds (see ExtremaLaunch)
+};
+
 struct GaussLaunch {
   int o;
+  int fuse;           // 1: extrema decisions of this octave in the same pass (X fields)
+  FusedExtrema X;
   float* gauss;       // plane (o, 0) of the Gaussian pyramid, nullptr = do not store
   float* dog;         // plane (o, 0) of the DoG pyramid
   double* next_seed;  // base of octave o+1 (nullptr for the last octave)
@@ -60,6 +78,8 @@ struct EmitLaunch {
   int row_off[kMaxOctaves + 1];  // first global row of each octave ([S][h] rows per octave)
   long long word_off[kMaxOctaves];  // first bitmap word of each octave
   int nw[kMaxOctaves];
+  int ww[kMaxOctaves];           // columns per bitmap word: kXW (scan) or kFX (fused)
+  int woff[kMaxOctaves];         // column of bit 0 of word 0: 0 (scan) or 1 (fused)
   const unsigned long long* bitmap;
   const unsigned* rowcount;      // [all rows]
   const unsigned* rowoff;        // exclusive scan of rowcount
@@ -100,6 +120,8 @@ size_t gauss_lds_bytes(const Pyramid& P, int o);
 bool gauss_needs_base0(const Pyramid& P);
 hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st);
 hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st);
+// Tile columns of a fused launch over a w-column octave (= bitmap words per row).
+inline int fused_words_per_row(int w) { return w > 2 ? (w - 2 + kFX - 1) / kFX : 1; }
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
 
 // Fills the unit table of L (octave geometry) and launches the scan; returns

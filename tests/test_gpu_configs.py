@@ -30,7 +30,7 @@ from sift_amd.synth import blob_image
 pytestmark = pytest.mark.gpu
 
 
-def _vs_oracle(ctx, img, p, mode):
+def _vs_oracle(ctx, img, p, mode, low_rtol=0.0):
     t0 = time.perf_counter()
     kp = ctx.detect(img, p).copy()
     cand = ctx.candidates()
@@ -41,7 +41,8 @@ def _vs_oracle(ctx, img, p, mode):
     print("\n%dx%d O%d S%d: GPU %.2f s, oracle (%s, %d threads) %.1f s: %d candidates, %d keypoints, %d low, "
           "%d exact fp64 re-decisions"
           % (img.shape[1], img.shape[0], p.num_octaves, p.scales_per_octave, t1 - t0,
-             "2D" if mode == orc.CONV_2D else "separable", host_threads(), t2 - t1, cand.shape[0], kp.shape[0],
+             {orc.CONV_2D: "2D", orc.CONV_SEPARABLE: "separable"}.get(mode, "gpu order"), host_threads(), t2 - t1,
+             cand.shape[0], kp.shape[0],
              r.n_low, counts["exact"]))
     if kp.shape[0] == r.refined.shape[0]:
         got = np.stack([kp["abs_sigma"], kp["abs_x"], kp["abs_y"]], 1)
@@ -50,7 +51,7 @@ def _vs_oracle(ctx, img, p, mode):
             float(np.abs(kp["interp_value"] - r.refined[:, 7]).max(initial=0.0))))
     check_candidates(cand, r.candidates())
     check_keypoints(kp, r.refined)
-    assert counts["low_contrast"] == r.n_low
+    assert abs(counts["low_contrast"] - r.n_low) <= low_rtol * r.n_low, (counts["low_contrast"], r.n_low)
     assert counts["singular"] == r.n_singular == 0
     return kp, r
 
@@ -103,7 +104,30 @@ def test_cfg5_8k_o6_s5_whole_vs_8_row_band_shards(gpu_ctx, img8k):
 
 
 @pytest.mark.timeout(900)
-def test_cfg5_8k_o6_s5_matches_oracle(gpu_ctx, img8k):
-    """The whole 8K image against the oracle (separable form)."""
-    kp, _ = _vs_oracle(gpu_ctx, img8k, sift_amd.make_params(6, 5), orc.CONV_SEPARABLE)
+@pytest.mark.parametrize("mode", [orc.CONV_SEPARABLE, orc.CONV_SEPARABLE_FMA_VH], ids=["separable", "gpu_order"])
+def test_cfg5_8k_o6_s5_matches_oracle(gpu_ctx, img8k, mode):
+    """The whole 8K image against the oracle.  Candidates and keypoints must
+    be identical in both summation orders.  The low-contrast count is exact
+    against the oracle in the HIP path's own operation order (columns then
+    rows, fma chains); against the rows-first order it may differ by a few of
+    ~435 K: low-contrast extrema in flat regions whose 26 neighbours tie to
+    the last fp64 bit, which either summation order may break (the reference's
+    2D order is a third one; 4K matches it exactly, above)."""
+    kp, _ = _vs_oracle(gpu_ctx, img8k, sift_amd.make_params(6, 5), mode,
+                       low_rtol=0.0 if mode == orc.CONV_SEPARABLE_FMA_VH else 1e-5)
     assert kp.shape[0] > 1000000
+
+
+@pytest.mark.parametrize("W,H,O,S,seed", [(640, 480, 5, 5, 3), (333, 517, 4, 3, 4)])
+def test_planes_bit_exact_in_gpu_order(gpu_ctx, W, H, O, S, seed):
+    """Every Gaussian and DoG plane is the fp32 rounding of the oracle's fp64
+    value computed in the HIP path's operation order, bit for bit."""
+    img = blob_image(W, H, seed=seed)
+    p = sift_amd.make_params(O, S)
+    gpu_ctx.build_scale_space(img, p)
+    r = orc.OracleRun(img, oracle_params(p), orc.CONV_SEPARABLE_FMA_VH, threads=host_threads())
+    for o, (h, w) in enumerate(r.dims):
+        for s in range(S + 3):
+            np.testing.assert_array_equal(gpu_ctx.plane(sift_amd.PLANE_GAUSS, o, s), r.gauss[o][s].astype(np.float32))
+        for s in range(S + 2):
+            np.testing.assert_array_equal(gpu_ctx.plane(sift_amd.PLANE_DOG, o, s), r.dog[o][s].astype(np.float32))
