@@ -57,7 +57,10 @@ enum {
   SIFT_F_SKIP_GAUSS_PLANES = 1 << 0, /* do not materialise Gaussian planes (seeds still kept) */
   SIFT_F_SKIP_DOG_PLANES = 1 << 1,   /* reserved: DoG planes are needed by refinement today   */
   SIFT_F_EXPORT_NEXT_SEED = 1 << 2,  /* also form the fp64 base of octave num_octaves (sift_next_seed) */
-  SIFT_F_KEYPOINT_ORIGINS = 1 << 3   /* record each keypoint's candidate (sift_keypoint_origins) */
+  SIFT_F_KEYPOINT_ORIGINS = 1 << 3,  /* record each keypoint's candidate (sift_keypoint_origins) */
+  SIFT_F_FUSED_EXTREMA = 1 << 4      /* detections: decide octave 0's extrema inside its Gaussian+DoG
+                                        pass instead of re-reading its DoG planes (same results;
+                                        measured slower on MI355X) */
 };
 
 /* Parameters of the pipeline.  Names and defaults follow

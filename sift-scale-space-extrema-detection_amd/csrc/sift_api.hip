@@ -86,7 +86,10 @@ struct sift_ctx {
   bool has_xseed = false;
   bool has_origins = false; // kp_key holds the candidate key of every keypoint
   std::vector<long long> x_word_off, x_row_off;
+  std::vector<int> x_nw, x_ww, x_woff;  // bitmap words per row, columns per word, column of bit 0
   long long x_rows = 0;
+  int x_nf = 0;             // leading octaves whose extrema decisions run fused into the Gaussian pass
+  bool x_prepared = false;  // extrema_prepare already ran for this detection (fused octaves)
   // device memory
   DBuf img, seeds, gauss, dog, wts;
   DBuf base0;                                  // materialised octave-0 base (large radii only)
@@ -374,17 +377,27 @@ static long long total_plane_px(const sift_ctx* ctx) {
   return t;
 }
 
-static int extrema_prepare(sift_ctx* ctx, hipStream_t st);
+static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf = 0);
 static int extrema_scan(sift_ctx* ctx, int o0, int o1, hipStream_t st);
+
+// Fused extrema decisions (k_gauss_dog, XF): SIFT_F_FUSED_EXTREMA, or
+// SIFT_FUSE=1 for every detection (experiments).
+static bool fuse_enabled(const sift_params* p) {
+  static const bool env = [] { const char* e = std::getenv("SIFT_FUSE"); return e && std::atoi(e) != 0; }();
+  return env || (p->flags & SIFT_F_FUSED_EXTREMA);
+}
 
 // overlap_extrema: launch each octave's extrema scan on the side stream as
 // soon as its DoG planes exist, overlapping the next octaves' Gaussian
 // kernels (memory-bound scans beside FMA-bound small octaves).
 // o_first > 0 (sift_detect_from_seed): no image; the fp64 base of octave
 // o_first is seed_host / seed_dev and octaves o_first .. O-1 are built.
+// fuse_extrema: a detection -- octave 0's extrema decisions run inside its
+// Gaussian+DoG launch (the extrema stage then scans octaves >= 1 only).
 static int build_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
                         size_t stride, const sift_params* p, const double* sig, bool overlap_extrema = false,
-                        int o_first = 0, const double* seed_host = nullptr, const double* seed_dev = nullptr) {
+                        int o_first = 0, const double* seed_host = nullptr, const double* seed_dev = nullptr,
+                        bool fuse_extrema = false) {
   if (!ctx) return SIFT_E_ARG;
   if (o_first == 0 && !img_host && !img_dev) return set_err(ctx, SIFT_E_ARG, "null image");
   if (o_first > 0 && !seed_host && !seed_dev) return set_err(ctx, SIFT_E_ARG, "null seed");
@@ -430,7 +443,15 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     base0 = ctx->base0.as<double>();
   }
   ctx->scans_done = false;
+  ctx->x_prepared = false;
   const bool overlap = overlap_extrema && ctx->side;
+  const int nf = (fuse_extrema && !overlap && o_first == 0 && fuse_enabled(p) && gauss_can_fuse(P, 0)) ? 1 : 0;
+  if (nf) {  // bitmap geometry, counter resets: before the fused launch writes them
+    ctx->dog_source = kNative;
+    rc = extrema_prepare(ctx, ctx->stream, nf);
+    if (rc) return rc;
+    ctx->x_prepared = true;
+  }
   if (overlap) {  // the side stream starts after this image's setup, resets the extrema counters
     ctx->dog_source = kNative;
     HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
@@ -454,6 +475,18 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.next_seed = (o + 1 < P.O) ? ctx->seeds.as<double>() + P.oct[o + 1].seed_off
                                 : (xseed ? ctx->xseed.as<double>() : nullptr);
     L.next_w = (o + 1 < P.O) ? P.oct[o + 1].w : (xseed ? ctx->xseed_w : 0);
+    if (o < nf) {
+      const ExtremaLaunch& XL = ctx->xl;
+      L.fuse = 1;
+      L.X.bitmap = XL.bitmap + XL.word_off[o];
+      L.X.rowcount = XL.rowcount + XL.row_off[o];
+      L.X.nw = ctx->x_nw[o];
+      L.X.amb_keys = XL.amb_keys;
+      L.X.counters = XL.counters;
+      L.X.amb_cap = XL.amb_cap;
+      L.X.c_lo = XL.c_lo;
+      L.X.c_hi = XL.c_hi;
+    }
     hipStream_t ls = ctx->stream;
     if (o == 0 && ctx->hi) {  // octave 0 on the high-priority stream, joined back
       HIPCHK(hipEventRecord(ctx->ev_hi_fork, ctx->stream));
@@ -646,16 +679,26 @@ constexpr int kRetry = 1;  // internal: a capacity overflowed, grow and run agai
 //   extrema_finish   row-count scan, ordered emission into cand_cap slots,
 //                    exact tie resolution (context stream).
 // Counts stay on the device.
-static int extrema_prepare(sift_ctx* ctx, hipStream_t st) {
+static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   Pyramid& P = ctx->P;
   const bool exact_planes = ctx->dog_source == kForeign;
   unsigned* cnt = ctx->counters.as<unsigned>();
-  // Row / word geometry of the candidate bitmap.
+  // Row / word geometry of the candidate bitmap: octaves < nf are decided in
+  // the Gaussian pass (kFX-column words, bit 0 = column 1), the rest by the
+  // scan (kXW-column words, bit 0 = column 0).
+  ctx->x_nf = nf;
   ctx->x_word_off.assign(P.O, 0);
   ctx->x_row_off.assign(P.O, 0);
+  ctx->x_nw.assign(P.O, 0);
+  ctx->x_ww.assign(P.O, 0);
+  ctx->x_woff.assign(P.O, 0);
   long long words = 0, rows = 0;
   for (int o = 0; o < P.O; ++o) {
-    const int nw = extrema_words_per_row(P.oct[o].w);
+    const bool f = o < nf;
+    const int nw = f ? fused_words_per_row(P.oct[o].w) : extrema_words_per_row(P.oct[o].w);
+    ctx->x_nw[o] = nw;
+    ctx->x_ww[o] = f ? kFX : kXW;
+    ctx->x_woff[o] = f ? 1 : 0;
     ctx->x_word_off[o] = words;
     ctx->x_row_off[o] = rows;
     words += (long long)P.S * P.oct[o].h * nw;
@@ -722,7 +765,9 @@ static int extrema_finish(sift_ctx* ctx) {
     for (int o = 0; o < P.O; ++o) {
       E.row_off[o] = (int)ctx->x_row_off[o];
       E.word_off[o] = ctx->x_word_off[o];
-      E.nw[o] = extrema_words_per_row(P.oct[o].w);
+      E.nw[o] = ctx->x_nw[o];
+      E.ww[o] = ctx->x_ww[o];
+      E.woff[o] = ctx->x_woff[o];
     }
     E.row_off[P.O] = (int)rows;
     E.bitmap = ctx->bitmap.as<unsigned long long>();
@@ -754,9 +799,15 @@ static int extrema_finish(sift_ctx* ctx) {
 // The whole extrema stage on the context stream.
 static int launch_extrema_stage(sift_ctx* ctx) {
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  int rc = extrema_prepare(ctx, ctx->stream);
-  if (rc) return rc;
-  rc = extrema_scan(ctx, ctx->o_first, ctx->P.O, ctx->stream);
+  int o0 = ctx->o_first;
+  if (ctx->x_prepared) {  // octaves < x_nf were decided in the Gaussian pass
+    ctx->x_prepared = false;
+    o0 = std::max(o0, ctx->x_nf);
+  } else {
+    const int rc = extrema_prepare(ctx, ctx->stream, 0);
+    if (rc) return rc;
+  }
+  int rc = extrema_scan(ctx, o0, ctx->P.O, ctx->stream);
   if (rc) return rc;
   return extrema_finish(ctx);
 }
@@ -1020,7 +1071,7 @@ int sift_refine(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out, si
 static int detect_begin(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H, size_t stride,
                         const sift_params* p) {
   if (!ctx) return SIFT_E_ARG;
-  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, true);
+  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, true, 0, nullptr, nullptr, true);
   if (rc) return rc;
   ctx->begin_pending = true;
   ctx->detect_host_img = img_host != nullptr;

@@ -10,6 +10,9 @@
 
 namespace sift {
 
+constexpr int kExactBatch = 16;  // <= kWPad: the zero taps after a weight vector cover a partial batch
+static_assert(kExactBatch <= kWPad, "batched taps stay inside the zero padding");
+
 // LDS doubles one wave needs: 4 L-scales x 3 rows x (2R+3) vertical sums.
 __host__ __device__ inline int exact_scratch_doubles(int rmax) { return 12 * (2 * rmax + 3) + 36; }
 
@@ -38,8 +41,17 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int o, int s, int y, int
     const int a = li / nc, c = li - nc * a;
     const int xx = clampi(x - 1 - r + c, 0, w - 1);
     const int yb = y - 1 + a - r;
+    // 16 loads in flight ahead of their fmas (the chain is latency bound
+    // otherwise); taps past 2r are the zero padding of wts: fma(0, v, acc) ==
+    // acc, so the sum is the same chain, bit for bit.
     double acc = 0.0;
-    for (int j = 0; j <= 2 * r; ++j) acc = fma(wp[j], base_at(P, o, clampi(yb + j, 0, h - 1), xx), acc);
+    for (int jb = 0; jb <= 2 * r; jb += kExactBatch) {
+      double v[kExactBatch];
+#pragma unroll
+      for (int k = 0; k < kExactBatch; ++k) v[k] = base_at(P, o, clampi(yb + jb + k, 0, h - 1), xx);
+#pragma unroll
+      for (int k = 0; k < kExactBatch; ++k) acc = fma(wp[jb + k], v[k], acc);
+    }
     sh[idx] = acc;
   }
   __syncthreads();

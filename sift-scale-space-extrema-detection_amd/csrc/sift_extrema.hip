@@ -26,51 +26,13 @@
 
 #include "sift_exact.h"
 #include "sift_kernels.h"
+#include "sift_xmask.h"
 
 #ifndef SIFT_XLOAD_AUX
 #define SIFT_XLOAD_AUX 0  // cache-policy bits of the scan's DoG loads (gfx950: 1 sc0, 2 nt, 16 sc1)
 #endif
 
 namespace sift {
-
-__device__ __forceinline__ unsigned lane_prefix(unsigned long long mask) {
-  return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-}
-
-// Wave-aggregated append: returns this lane's slot (valid where pred).
-__device__ __forceinline__ unsigned wave_append(bool pred, unsigned* counter) {
-  const unsigned long long mask = __ballot(pred);
-  if (mask == 0ull) return 0u;
-  const int leader = __ffsll((long long)mask) - 1;
-  unsigned base = 0u;
-  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, (unsigned)__popcll(mask));
-  base = __shfl(base, leader);
-  return base + lane_prefix(mask);
-}
-
-// Lane l-1 / lane l+1 of a wave (DPP wave shifts; lanes 0 / 63 get 0, they
-// are halo lanes whose results are never used).
-__device__ __forceinline__ float from_left(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float from_right(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
-}
-
-__device__ __forceinline__ float max3f(float a, float b, float c) { return __builtin_fmaxf(a, __builtin_fmaxf(b, c)); }
-__device__ __forceinline__ float min3f(float a, float b, float c) { return __builtin_fminf(a, __builtin_fminf(b, c)); }
-
-// Per-wave state of the 3-row window over NP consecutive DoG planes (the
-// centre planes 1..NP-2 are scales, 0 and NP-1 their outer neighbours).
-// Slot k holds the row whose offset from the group's first centre row is
-// k mod 3; all indices are compile-time constants, so nothing rotates.
-template <int NP>
-struct XWin {
-  float hx[3][NP], hn[3][NP];  // 3-wide max / min of a row
-  float ex[3][NP], en[3][NP];  // 2-wide (x-1, x+1) max / min (centre planes)
-  float cv[3][NP];             // the value (centre planes)
-  float raw[3][NP];            // loaded, not yet derived rows
-};
 
 template <int NP>
 struct XUnit {
@@ -99,28 +61,6 @@ __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int
                                            SIFT_XLOAD_AUX));
 }
 
-template <int NP, int K>
-__device__ __forceinline__ void x_derive(XWin<NP>& Wn, const float (&src)[NP]) {
-#if defined(SIFT_X_PROBE) && SIFT_X_PROBE > 1  // timing probe: loads only
-#pragma unroll
-  for (int q = 0; q < NP; ++q) { Wn.hx[K][q] = src[q]; Wn.hn[K][q] = src[q]; }
-  return;
-#endif
-#pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const float v = src[q];
-    const float l = from_left(v), r = from_right(v);
-    const float m2 = __builtin_fmaxf(l, r), n2 = __builtin_fminf(l, r);
-    Wn.hx[K][q] = __builtin_fmaxf(m2, v);
-    Wn.hn[K][q] = __builtin_fminf(n2, v);
-    if (q >= 1 && q <= NP - 2) {
-      Wn.ex[K][q] = m2;
-      Wn.en[K][q] = n2;
-      Wn.cv[K][q] = v;
-    }
-  }
-}
-
 // Centre row y (slots A = y-1, B = y, C = y+1): decide every scale of the group.
 template <int NP, int A, int B, int C>
 __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const ExtremaLaunch& L, int y) {
@@ -145,33 +85,16 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     const float v = Wn.cv[B][q];
     const float nmax = max3f(vx[q - 1], vx[q + 1], max3f(Wn.hx[A][q], Wn.hx[C][q], Wn.ex[B][q]));
     const float nmin = min3f(vn[q - 1], vn[q + 1], min3f(Wn.hn[A][q], Wn.hn[C][q], Wn.en[B][q]));
-    // Lane masks (SALU from here on).  Most rows of a 62-column word hold no
-    // extremum at a given scale: one ballot decides, the rest is skipped.
-    const unsigned long long ext_any = __ballot(v >= nmax || v <= nmin) & U.colmask;
-    if (ext_any) {
-      const float av = __builtin_fabsf(v);
-      const unsigned long long gt = __ballot(v > nmax), lt = __ballot(v < nmin);
-      const unsigned long long lo = __ballot(av < L.c_lo), hi = __ballot(av >= L.c_hi);
-      const unsigned long long certain = (gt | lt) & U.colmask;
-      unsigned long long ext, tie;
-      if (L.exact_planes) { ext = certain; tie = 0ull; }
-      else { ext = ext_any; tie = ext & ~certain; }
-      const unsigned long long count_low = ext & lo & ~tie;
-      const unsigned long long bit = ext & ~count_low;
-      const unsigned long long amb = bit & (tie | ~hi);
-      U.low += (unsigned)__popcll(count_low);
+    const unsigned key = U.key_base + (unsigned)(q - 1) * (unsigned)U.plane + (unsigned)y * (unsigned)U.w +
+                         (unsigned)(U.xw * kXW - 1 + U.lane);
+    const unsigned long long bit = x_row_decide(v, nmax, nmin, U.colmask, L.c_lo, L.c_hi, L.exact_planes != 0, key,
+                                                &L.counters[0], L.amb_keys, L.amb_cap, U.low);
+    if (bit) {
       const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
       if (U.lane == q - 1) {
         wlo = (unsigned)word;
         whi = (unsigned)(word >> 32);
         wcnt = (unsigned)__popcll(word);
-      }
-      if (amb) {  // rare: ties / contrast within fp32 rounding of the threshold
-        const bool mine = (amb >> U.lane) & 1ull;
-        const unsigned slot = wave_append(mine, &L.counters[0]);
-        if (mine && slot < L.amb_cap)
-          L.amb_keys[slot] = U.key_base + (unsigned)(q - 1) * (unsigned)U.plane + (unsigned)y * (unsigned)U.w +
-                             (unsigned)(U.xw * kXW - 1 + U.lane);
       }
     }
   }
@@ -301,10 +224,11 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
       if (lane >= off) inc += t;
     }
     unsigned pos = base + inc - c;
+    const int xb = xw * E.ww[o] + E.woff[o];  // column of bit 0
     while (word) {
       const int b = __ffsll((long long)word) - 1;
       word &= word - 1;
-      const int x = xw * kXW + b;
+      const int x = xb + b;
       if (pos < E.cap) {
         E.keys[pos] = kbase + (unsigned)x;
         E.value[pos] = (double)Dc[x];

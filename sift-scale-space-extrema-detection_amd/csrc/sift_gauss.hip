@@ -49,6 +49,7 @@
 
 #include "sift_common.h"
 #include "sift_kernels.h"
+#include "sift_xmask.h"
 
 #include <vector>
 
@@ -103,6 +104,15 @@ __device__ __forceinline__ void pin(double (&a)[N]) {
 // execute in order, so waiting for its own outstanding ones (and keeping the
 // compiler from moving LDS accesses across) is all the ordering needed.
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Block barrier that orders LDS only: __syncthreads() is a release/acquire
+// fence at workgroup scope and would also wait for every outstanding plane
+// store of the wave (they are fire-and-forget otherwise).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ double load_f64(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
@@ -435,9 +445,87 @@ __device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t rs, int voff, con
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f), rs, voff, 0, SIFT_STORE_AUX);
 }
 
+// ---------------------------------------------------------------------------
+// Extrema decisions fused into the pass (XF).  Tiles overlap: a block
+// computes 64 x 32 pixels at a stride of kFX x kFY, stores the kFX x kFY it
+// owns (the last tile of a row / column all of its in-plane pixels) and
+// decides the kFX x kFY pixels one column and one row in from its origin,
+// whose 26 neighbours all lie in its tile (translation invariance makes the
+// overlapping pixels bit-identical to their owners').  Each scale's DoG tile
+// goes to an LDS ring of 3 fp32 planes; once DoG t+1 is there, every wave
+// decides scale t for its own rows with the scan's logic (x_row_decide:
+// fp32 comparisons, ties and threshold-adjacent values to the exact pass).
+// Replaces the scan of this octave: its DoG planes are not read back.
+// ---------------------------------------------------------------------------
+constexpr int kRingPlane = kGY * kGX;  // floats per ring plane
+
+// Scale t (DoG t-1, t, t+1 in ring slots (t-1)%3, t%3, (t+1)%3) for the
+// wave's rows 8 wv .. 8 wv + 7; one lane per tile column.
+__device__ __forceinline__ void fused_decide(const Pyramid& P, const GaussLaunch& L, const GTile& T,
+                                             const float* ring, int t, unsigned& low) {
+  const Octave& oc = P.oct[L.o];
+  const int l = T.lane;
+  const float* q0 = ring + ((t - 1) % 3) * kRingPlane + l;
+  const float* q1 = ring + (t % 3) * kRingPlane + l;
+  const float* q2 = ring + ((t + 1) % 3) * kRingPlane + l;
+  const int x = T.x0 + l;
+  const unsigned long long colmask = __ballot(l >= 1 && l <= kFX && x >= 1 && x <= T.w - 2);
+  const unsigned key0 = oc.key_off + (unsigned)(t - 1) * (unsigned)T.h * (unsigned)T.w + (unsigned)x;
+  const int r0 = 8 * T.wv;
+  XWin<3> Wn;
+  auto load = [&](float (&dst)[3], int j) {  // tile row r0 - 1 + j (clamped: only undecided rows read past)
+    const int r = clampi(r0 - 1 + j, 0, kGY - 1) * kGX;
+    dst[0] = q0[r];
+    dst[1] = q1[r];
+    dst[2] = q2[r];
+  };
+  {
+    float a[3], b[3];
+    load(a, 0);
+    load(b, 1);
+    x_derive<3, 0>(Wn, a);
+    x_derive<3, 1>(Wn, b);
+  }
+  auto centre = [&](auto A_, auto B_, auto C_, int j) {
+    constexpr int A = decltype(A_)::value, B = decltype(B_)::value, C = decltype(C_)::value;
+    const int c = r0 + j - 1;  // tile row of the centre
+    const int y = T.y0 + c;
+    if (c < 1 || c > kFY || y < 1 || y > T.h - 2) return;  // wave-uniform
+    const float vx0 = max3f(Wn.hx[A][0], Wn.hx[B][0], Wn.hx[C][0]), vn0 = min3f(Wn.hn[A][0], Wn.hn[B][0], Wn.hn[C][0]);
+    const float vx2 = max3f(Wn.hx[A][2], Wn.hx[B][2], Wn.hx[C][2]), vn2 = min3f(Wn.hn[A][2], Wn.hn[B][2], Wn.hn[C][2]);
+    const float v = Wn.cv[B][1];
+    const float nmax = max3f(vx0, vx2, max3f(Wn.hx[A][1], Wn.hx[C][1], Wn.ex[B][1]));
+    const float nmin = min3f(vn0, vn2, min3f(Wn.hn[A][1], Wn.hn[C][1], Wn.en[B][1]));
+    const unsigned long long bit =
+        x_row_decide(v, nmax, nmin, colmask, L.X.c_lo, L.X.c_hi, false, key0 + (unsigned)y * (unsigned)T.w,
+                     &L.X.counters[0], L.X.amb_keys, L.X.amb_cap, low);
+    const unsigned long long word = bit >> 1;  // lanes 1..kFX -> bits 0..kFX-1
+    if (l == 0) {
+      const long long row = (long long)(t - 1) * T.h + y;
+      L.X.bitmap[row * L.X.nw + blockIdx.x] = word;
+      if (word) atomicAdd(&L.X.rowcount[row], (unsigned)__popcll(word));
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  // rows j = 2..9 are derived into slot j % 3, centre row j - 1 uses slots (j-2, j-1, j) % 3
+  {
+    float a[3];
+    load(a, 2); x_derive<3, 2>(Wn, a); centre(I0{}, I1{}, I2{}, 1);
+    load(a, 3); x_derive<3, 0>(Wn, a); centre(I1{}, I2{}, I0{}, 2);
+    load(a, 4); x_derive<3, 1>(Wn, a); centre(I2{}, I0{}, I1{}, 3);
+    load(a, 5); x_derive<3, 2>(Wn, a); centre(I0{}, I1{}, I2{}, 4);
+    load(a, 6); x_derive<3, 0>(Wn, a); centre(I1{}, I2{}, I0{}, 5);
+    load(a, 7); x_derive<3, 1>(Wn, a); centre(I2{}, I0{}, I1{}, 6);
+    load(a, 8); x_derive<3, 2>(Wn, a); centre(I0{}, I1{}, I2{}, 7);
+    load(a, 9); x_derive<3, 0>(Wn, a); centre(I1{}, I2{}, I0{}, 8);
+  }
+}
+
 // SWC > 0: compile-time strip stride (immediate LDS offsets); 0: L.sw.
-// RMAX: radii with unrolled code.
-template <bool OCT0, int SWC, int RMAX>
+// RMAX: radii with unrolled code.  XF: extrema decisions fused (above).
+template <bool OCT0, int SWC, int RMAX, bool XF>
 __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const Octave& oc = P.oct[L.o];
@@ -445,8 +533,8 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   GTile T;
   T.h = oc.h;
   T.w = oc.w;
-  T.x0 = bx * kGX;
-  T.y0 = by * kGY;
+  T.x0 = bx * (XF ? kFX : kGX);
+  T.y0 = by * (XF ? kFY : kGY);
   T.lane = threadIdx.x & 63;
   T.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   T.cg = T.lane & (kCG - 1);
@@ -460,6 +548,11 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   const int nstrip = kGY * T.sw;
   T.S0 = smem + nstrip;
   double* V = smem;
+  // fused extrema: fp32 DoG ring after the strip and the staged region
+  float* ring = nullptr;
+  if constexpr (XF)
+    ring = reinterpret_cast<float*>(smem + nstrip + (OCT0 ? (fl2(kGY - 1 + oc.rmax) + T.hrm + 1) * kBW0 : 0));
+  unsigned xlow = 0;
 
   // The generic horizontal path reads (with zero taps) past the columns a
   // scale writes: those must be finite.
@@ -481,13 +574,19 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   const long long plane = (long long)T.h * T.w;
   const int x = T.x0 + 4 * T.cg;
   const int nvalid = T.w - x;
-  // Per-lane byte offsets of its two output rows in a plane (past the plane:
-  // the store is dropped).
+  // Pixels this block stores: all of its tile, or with fused extrema the
+  // kFX x kFY it owns (the last tile of a row / column: all it computes).
+  const bool own_c = !XF || 4 * T.cg < kFX || bx == (int)gridDim.x - 1;
+  bool own[kNR];
+  // Per-lane byte offsets of its two output rows in a plane (past the plane
+  // or not owned: the store is dropped).
   int voff[kNR];
 #pragma unroll
   for (int i = 0; i < kNR; ++i) {
-    const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
-    voff[i] = (y < T.h && nvalid > 0) ? (y * T.w + x) * 4 : 0x7ffffff0;
+    const int r = 8 * T.wv + T.rs + kRS * i;
+    const int y = T.y0 + r;
+    own[i] = y < T.h && nvalid > 0 && own_c && (!XF || r < kFY || by == (int)gridDim.y - 1);
+    voff[i] = own[i] ? (y * T.w + x) * 4 : 0x7ffffff0;
   }
 
   // Scale group of this block (small octaves split their scales over
@@ -512,12 +611,12 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     horz_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V, out);
     wave_lds_fence();  // strip rows read before the next scale overwrites them
 
+    double d[kNR][4];
+#pragma unroll
+    for (int i = 0; i < kNR; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
     if (s >= s_begin && (st || out[0][0] == 12345.0)) {
-      double d[kNR][4];
-#pragma unroll
-      for (int i = 0; i < kNR; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
       if (L.vec) {
         const unsigned pb = (unsigned)plane * 4u;
         if (L.gauss) {
@@ -534,7 +633,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
 #pragma unroll
         for (int i = 0; i < kNR; ++i) {
           const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
-          if (y < T.h && nvalid > 0) {
+          if (own[i]) {
             const long long pp = (long long)y * T.w + x;
             if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
             if (s > 0) store4(L.dog + (s - 1) * plane + pp, d[i], nvalid);
@@ -542,11 +641,28 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
         }
       }
     }
+    if constexpr (XF) {
+      // DoG s-1 into ring slot (s-1) % 3, then decide scale s-2 once DoG
+      // s-3, s-2, s-1 are all there (scales 1..S; s runs to S+2).
+      if (s >= 1) {
+        if (s >= 4) lds_barrier();  // the decision of scale s-3 has read slot (s-1) % 3
+#pragma unroll
+        for (int i = 0; i < kNR; ++i) {
+          const float4 f = make_float4((float)d[i][0], (float)d[i][1], (float)d[i][2], (float)d[i][3]);
+          *reinterpret_cast<float4*>(ring + ((s - 1) % 3) * kRingPlane + (8 * T.wv + T.rs + kRS * i) * kGX +
+                                     4 * T.cg) = f;
+        }
+        if (s >= 3) {
+          lds_barrier();  // every wave's rows of DoG s-1 are in the ring
+          if (!(L.dbg & 2)) fused_decide(P, L, Ts, ring, s - 2, xlow);  // dbg 2: timing without the decisions
+        }
+      }
+    }
     if (s == P.S && L.next_seed && s >= s_begin) {
 #pragma unroll
       for (int i = 0; i < kNR; ++i) {
         const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
-        if (y < T.h && nvalid > 0 && !(y & 1)) {
+        if (own[i] && !(y & 1)) {
           double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
           sd[0] = out[i][0];
           if (nvalid > 2) sd[1] = out[i][2];
@@ -557,6 +673,9 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     for (int i = 0; i < kNR; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
+  }
+  if constexpr (XF) {
+    if (T.lane == 0 && xlow) atomicAdd(&L.X.counters[1], xlow);
   }
 }
 
@@ -606,8 +725,16 @@ static size_t staged_bytes(const Pyramid& P, int o) {
   return sizeof(double) * (size_t)(fl2(kGY - 1 + R) + cl2(R) + 1) * kBW0;
 }
 
-size_t gauss_lds_bytes(const Pyramid& P, int o) {
-  return sizeof(double) * kGY * strip_stride(P, o) + staged_bytes(P, o);
+size_t gauss_lds_bytes(const Pyramid& P, int o, bool fused) {
+  return sizeof(double) * kGY * strip_stride(P, o) + staged_bytes(P, o) +
+         (fused ? sizeof(float) * 3 * kRingPlane : 0);
+}
+
+bool gauss_can_fuse(const Pyramid& P, int o) {
+  const Octave& oc = P.oct[o];
+  // staged0 implies octave 0, which never splits its scales (scale_groups)
+  return staged0(P, o) && oc.h >= 3 && oc.w >= 3 && P.S >= 1 &&
+         gauss_lds_bytes(P, o, true) <= 160 * 1024;
 }
 
 // Cost of one scale of a tile, in units of one fp64 tap per output of both
@@ -674,9 +801,9 @@ static int scale_groups(const Pyramid& P, int o) {
   return g;
 }
 
-template <bool O0, int SWC, int RMAX>
+template <bool O0, int SWC, int RMAX, bool XF>
 static void set_attr() {
-  (void)hipFuncSetAttribute((const void*)k_gauss_dog<O0, SWC, RMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_gauss_dog<O0, SWC, RMAX, XF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
 }
 
@@ -689,15 +816,20 @@ hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st)
 
 hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
   const Octave& oc = P.oct[L.o];
+  if (L.fuse && !gauss_can_fuse(P, L.o)) return hipErrorInvalidValue;
   const int G = scale_groups(P, L.o);
   split_scales(P, L.o, G, L.gb);
-  dim3 grid((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, G);
-  const size_t lds = gauss_lds_bytes(P, L.o);
+  const dim3 grid = L.fuse ? dim3(fused_words_per_row(oc.w), (oc.h - 2 + kFY - 1) / kFY, 1)
+                           : dim3((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, G);
+  if (L.fuse && (int)grid.x != L.X.nw) return hipErrorInvalidValue;
+  const size_t lds = gauss_lds_bytes(P, L.o, L.fuse != 0);
   static bool attr_set = false;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    set_attr<true, kSW0, 8>();
-    set_attr<true, kSW1, kUR>();
-    set_attr<false, 0, kUR1>();
+    set_attr<true, kSW0, 8, false>();
+    set_attr<true, kSW1, kUR, false>();
+    set_attr<false, 0, kUR1, false>();
+    set_attr<true, kSW0, 8, true>();
+    set_attr<true, kSW1, kUR, true>();
     attr_set = true;
   }
   L.sw = strip_stride(P, L.o);
@@ -707,9 +839,16 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
                    (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
   L.vec = (a16 && (oc.w & 3) == 0 && 4.0 * oc.h * oc.w < 2147483648.0) ? 1 : 0;
   L.zero = oc.rmax > (staged0(P, L.o) ? kUR : kUR1) ? 1 : 0;
-  if (staged0(P, L.o) && L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8>), grid, dim3(256), lds, st, P, L);
-  else if (staged0(P, L.o)) hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR>), grid, dim3(256), lds, st, P, L);
-  else hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1>), grid, dim3(256), lds, st, P, L);
+  if (L.fuse) {  // staged octave 0 (gauss_can_fuse)
+    if (L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, true>), grid, dim3(256), lds, st, P, L);
+    else hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, true>), grid, dim3(256), lds, st, P, L);
+  } else if (staged0(P, L.o) && L.sw == kSW0) {
+    hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, false>), grid, dim3(256), lds, st, P, L);
+  } else if (staged0(P, L.o)) {
+    hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, false>), grid, dim3(256), lds, st, P, L);
+  } else {
+    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false>), grid, dim3(256), lds, st, P, L);
+  }
   return hipGetLastError();
 }
 

@@ -12,7 +12,10 @@ struct Keypoint {
   double abs_x, abs_y, abs_sigma, interp_value;
 };
 
-constexpr int kFX = 60;      // fused extrema: tile stride in x (64 computed columns, 60 owned, 60 decided)
+#ifndef SIFT_FX
+#define SIFT_FX 60
+#endif
+constexpr int kFX = SIFT_FX; // fused extrema: tile stride in x (64 computed columns, 60 owned, 60 decided)
 constexpr int kFY = 30;      // ... in y (32 computed rows, 30 owned, 30 decided)
 
 // Extrema decisions fused into the Gaussian+DoG pass of one octave (see
@@ -114,7 +117,10 @@ struct RefineLaunch {
   unsigned* counters; // [3] n uncertain, [4] n singular
 };
 
-size_t gauss_lds_bytes(const Pyramid& P, int o);
+size_t gauss_lds_bytes(const Pyramid& P, int o, bool fused = false);
+// Octave o can run with its extrema decisions fused (GaussLaunch.fuse):
+// octave 0 on the staged path, one scale group, a plane of at least 3 x 3.
+bool gauss_can_fuse(const Pyramid& P, int o);
 // Octave 0 radii above the unrolled range run on a materialised fp64 upsample
 // of the input (4 H W doubles) instead of the staged input region.
 bool gauss_needs_base0(const Pyramid& P);

@@ -50,8 +50,12 @@ struct StepOut {
 // alpha by 2^(o-1) -- 16 at octave 5 of an 8K pyramid, where the DoG values
 // are small and fp32 rounding of the planes moves alpha by ~1e-5 -- so a
 // keypoint whose bound exceeds this is recomputed from exact fp64 patches.
-constexpr double kKeypointTol = 2e-5;
+#ifndef SIFT_KP_TOL
+#define SIFT_KP_TOL 2e-5
+#endif
+constexpr double kKeypointTol = SIFT_KP_TOL;
 constexpr double kValueTol = 1e-7;  // interpolatedValue (the tests hold it to 1e-6)
+constexpr unsigned kPolish = 0x80000000u;  // uncertain-list entry: exact values at the final position only
 
 // One iteration of background.js:480-664 on the patch d[k][a][c]
 // (k: scale s-1+k, a: row m-1+a, c: col n-1+c).  `delta` bounds the error of
@@ -271,7 +275,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const int nb = (n + 255) / 256;
   if ((int)blockIdx.x >= nb) return;  // whole block past the live slots
   const int i = (SIFT_REFINE_XCD ? xcd_block(blockIdx.x, nb) : (int)blockIdx.x) * 256 + threadIdx.x;
-  bool unc = false;
+  bool unc = false, polish = false;
   if (i < n && L.keep && !L.keep[i]) {
     L.status[i] = kRefDiscard;
   } else if (i < n) {
@@ -318,8 +322,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
       if (R.state == 3) { status = kRefSingular; break; }
       if (R.state == 2) { status = kRefDiscard; break; }
       if (R.state == 1) {
-        if (R.imprecise) {  // decisions certain, output not precise enough: exact pass
-          unc = true;
+        if (R.imprecise) {  // decisions certain, output not precise enough: exact values at this position
+          unc = polish = true;
+          Keypoint& k = L.kp[i];  // the final position for the exact pass (it rewrites the record)
+          k.scale_level = s;
+          k.local_y = m;
+          k.local_x = n;
           atomicAdd(&L.counters[27], 1u);
           break;
         }
@@ -339,18 +347,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&L.counters[3], (unsigned)__popcll(mask));
     base = __shfl(base, leader);
     const unsigned pre = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-    if (unc) L.uncertain[base + pre] = (unsigned)i;
+    if (unc) L.uncertain[base + pre] = (unsigned)i | (polish ? kPolish : 0u);
   }
 }
 
 // One wave per uncertain candidate (persistent over the device-side count):
-// exact fp64 patches, lane 0 decides.
+// exact fp64 patches, lane 0 decides.  Polish entries (kPolish: every
+// decision of the fast pass was certain, only the kept keypoint's output was
+// not precise enough) recompute just the candidate's exact value (omega uses
+// it, background.js:565) and the final position's patch.
 __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const RefineLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int pos[4];
   const unsigned nu = min(L.counters[3], (unsigned)L.cap);
   for (unsigned j = blockIdx.x; j < nu; j += gridDim.x) {
-    const unsigned i = L.uncertain[j];
+    const unsigned e = L.uncertain[j];
+    const unsigned i = e & ~kPolish;
     int o, s, m, n;
     decode_key(P, L.cand_key[i], o, s, m, n);
     const Octave& oc = P.oct[o];
@@ -359,6 +371,27 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
     double* sh = smem + 32 + 40;
     double value = 0;
     int status = kRefDiscard;
+    if (e & kPolish) {
+      wave_dog_patch(P, o, s, m, n, sh, Lbuf, d27);
+      value = d27[13];  // all lanes: d27 is visible after the patch's barrier
+      const Keypoint& k = L.kp[i];
+      const int s1 = k.scale_level, m1 = k.local_y, n1 = k.local_x;
+      if (s1 != s || m1 != m || n1 != n) wave_dog_patch(P, o, s1, m1, n1, sh, Lbuf, d27);
+      if (threadIdx.x == 0) {
+        const StepOut R = refine_step<false>(d27, o, s1, m1, n1, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr,
+                                             false, 0.0);
+        pos[3] = R.state == 1;
+        if (R.state == 1) make_keypoint(L.kp[i], o, R, P.S, L.min_blur, L.min_interpixel_distance, (P.row0 * 2) >> o);
+      }
+      __syncthreads();
+      const bool done = pos[3];
+      __syncthreads();
+      if (done) {
+        if (threadIdx.x == 0) L.status[i] = kRefKeep;
+        continue;
+      }
+      // not kept on exact values (cannot happen with certain decisions): the whole chain
+    }
     for (int it = 0; it < 5; ++it) {
       wave_dog_patch(P, o, s, m, n, sh, Lbuf, d27);
       if (threadIdx.x == 0) {

@@ -29,6 +29,7 @@ PLANE_DOG = 1
 F_SKIP_GAUSS_PLANES = 1
 F_EXPORT_NEXT_SEED = 4
 F_KEYPOINT_ORIGINS = 8
+F_FUSED_EXTREMA = 16
 
 AFTER_OCTAVE0 = 0
 AFTER_GAUSSIAN = 1

@@ -131,3 +131,17 @@ def test_planes_bit_exact_in_gpu_order(gpu_ctx, W, H, O, S, seed):
             np.testing.assert_array_equal(gpu_ctx.plane(sift_amd.PLANE_GAUSS, o, s), r.gauss[o][s].astype(np.float32))
         for s in range(S + 2):
             np.testing.assert_array_equal(gpu_ctx.plane(sift_amd.PLANE_DOG, o, s), r.dog[o][s].astype(np.float32))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("W,H,O,S,seed", [(3840, 2160, 4, 5, 42), (333, 517, 4, 3, 4), (64, 48, 3, 3, 5)])
+def test_fused_extrema_flag_same_results(gpu_ctx, W, H, O, S, seed):
+    """SIFT_F_FUSED_EXTREMA (octave 0's decisions inside its Gaussian pass):
+    candidates, low-contrast count and keypoints identical to the scan."""
+    img = blob_image(W, H, seed=seed)
+    a = gpu_ctx.detect(img, sift_amd.make_params(O, S)).copy()
+    ca, na = gpu_ctx.candidates(), gpu_ctx.counts()
+    b = gpu_ctx.detect(img, sift_amd.make_params(O, S, flags=sift_amd.F_FUSED_EXTREMA)).copy()
+    cb, nb = gpu_ctx.candidates(), gpu_ctx.counts()
+    assert a.tobytes() == b.tobytes() and ca.tobytes() == cb.tobytes()
+    assert na["low_contrast"] == nb["low_contrast"] and na["candidates"] == nb["candidates"]

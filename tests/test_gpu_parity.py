@@ -23,6 +23,13 @@ from sift_amd.synth import blob_image
 
 pytestmark = pytest.mark.gpu
 
+
+def params_of(g, flags=0):
+    P = g.params
+    return sift_amd.make_params(P["num_octaves"], P["scales_per_octave"], P["min_blur"], P["assumed_blur"],
+                                P["min_interpixel_distance"], flags)
+
+
 @pytest.mark.parametrize("name", case_names())
 def test_detect_matches_reference(gpu_ctx, name):
     g = Golden(name)
