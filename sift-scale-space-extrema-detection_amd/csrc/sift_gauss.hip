@@ -81,6 +81,7 @@ __host__ __device__ constexpr int cl2(int a) { return (a + 1) >> 1; }  // ceil(a
 
 struct GTile {
   int h, w, x0, y0;
+  int bx;              // tile column
   int lane, wv;        // wv wave-uniform (SGPR)
   int cg, rs;          // horizontal mapping
   int sw;              // strip stride
@@ -502,7 +503,7 @@ __device__ __forceinline__ void fused_decide(const Pyramid& P, const GaussLaunch
     const unsigned long long word = bit >> 1;  // lanes 1..kFX -> bits 0..kFX-1
     if (l == 0) {
       const long long row = (long long)(t - 1) * T.h + y;
-      L.X.bitmap[row * L.X.nw + blockIdx.x] = word;
+      L.X.bitmap[row * L.X.nw + T.bx] = word;
       if (word) atomicAdd(&L.X.rowcount[row], (unsigned)__popcll(word));
     }
   };
@@ -529,8 +530,19 @@ template <bool OCT0, int SWC, int RMAX, bool XF>
 __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const Octave& oc = P.oct[L.o];
-  const int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  // 1D grid: block -> (scale group, tile).  Blocks are dispatched round-robin
+  // over the 8 XCDs; with xcd_band, XCD k runs the k-th contiguous range of
+  // tiles (a band of tile rows), so the base rows its vertical passes re-read
+  // stay in its own L2.  Groups of one tile are adjacent (same base region).
+  int lb = blockIdx.x;
+  if (L.xcd_band) {
+    const int nb = L.gx * L.gy * L.G, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    lb = xc * q + min(xc, rm) + (lb >> 3);
+  }
+  const int bz = lb % L.G, bt = lb / L.G;
+  const int bx = bt % L.gx, by = bt / L.gx;
   GTile T;
+  T.bx = bx;
   T.h = oc.h;
   T.w = oc.w;
   T.x0 = bx * (XF ? kFX : kGX);
@@ -576,7 +588,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   const int nvalid = T.w - x;
   // Pixels this block stores: all of its tile, or with fused extrema the
   // kFX x kFY it owns (the last tile of a row / column: all it computes).
-  const bool own_c = !XF || 4 * T.cg < kFX || bx == (int)gridDim.x - 1;
+  const bool own_c = !XF || 4 * T.cg < kFX || bx == L.gx - 1;
   bool own[kNR];
   // Per-lane byte offsets of its two output rows in a plane (past the plane
   // or not owned: the store is dropped).
@@ -585,7 +597,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   for (int i = 0; i < kNR; ++i) {
     const int r = 8 * T.wv + T.rs + kRS * i;
     const int y = T.y0 + r;
-    own[i] = y < T.h && nvalid > 0 && own_c && (!XF || r < kFY || by == (int)gridDim.y - 1);
+    own[i] = y < T.h && nvalid > 0 && own_c && (!XF || r < kFY || by == L.gy - 1);
     voff[i] = own[i] ? (y * T.w + x) * 4 : 0x7ffffff0;
   }
 
@@ -819,9 +831,16 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
   if (L.fuse && !gauss_can_fuse(P, L.o)) return hipErrorInvalidValue;
   const int G = scale_groups(P, L.o);
   split_scales(P, L.o, G, L.gb);
-  const dim3 grid = L.fuse ? dim3(fused_words_per_row(oc.w), (oc.h - 2 + kFY - 1) / kFY, 1)
-                           : dim3((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, G);
-  if (L.fuse && (int)grid.x != L.X.nw) return hipErrorInvalidValue;
+  L.gx = L.fuse ? fused_words_per_row(oc.w) : (oc.w + kGX - 1) / kGX;
+  L.gy = L.fuse ? (oc.h - 2 + kFY - 1) / kFY : (oc.h + kGY - 1) / kGY;
+  L.G = L.fuse ? 1 : G;
+  if (L.fuse && L.gx != L.X.nw) return hipErrorInvalidValue;
+  // XCD-banded tile order for octaves >= 1 (SIFT_XCD_BAND: bit o-1 of the
+  // value; default all).  Measured (4K, O=4, S=5): isolated pass 0.748 ->
+  // 0.730 ms, pipelined bench +0.5-1 % (tools/gpu_envab.sh).
+  static const int xband = [] { const char* e = std::getenv("SIFT_XCD_BAND"); return e ? std::atoi(e) : -1; }();
+  L.xcd_band = L.o >= 1 && ((xband >> (L.o - 1)) & 1);
+  const dim3 grid(L.gx * L.gy * L.G);
   const size_t lds = gauss_lds_bytes(P, L.o, L.fuse != 0);
   static bool attr_set = false;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)

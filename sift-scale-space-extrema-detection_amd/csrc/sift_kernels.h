@@ -45,7 +45,9 @@ struct GaussLaunch {
   int vec;            // float4 plane stores are aligned
   int zero;           // strips need zeroing (generic-radius path present)
   int dbg;            // timing experiments (SIFT_GAUSS_DBG): bit 0 = no plane stores
-  int gb[kMaxScales + 1];  // scale groups (blockIdx.z): group g computes scales gb[g] .. gb[g+1]-1
+  int gb[kMaxScales + 1];  // scale groups: group g computes scales gb[g] .. gb[g+1]-1
+  int gx, gy, G;      // tiles per row, tile rows, scale groups (1D grid of gx gy G blocks)
+  int xcd_band;       // 1: block -> tile so that each XCD runs a contiguous band of tile rows
 };
 
 constexpr int kXW = 62;      // output columns per extrema wave (lanes 1..62; lanes 0, 63 are halo)
