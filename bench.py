@@ -139,9 +139,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--width", type=int, default=3840)
-    ap.add_argument("--height", type=int, default=2160)
-    ap.add_argument("--octaves", type=int, default=4)
+    ap.add_argument("--width", type=int, default=None, help="default 3840 (7680 with --shard-image)")
+    ap.add_argument("--height", type=int, default=None, help="default 2160 (4320 with --shard-image)")
+    ap.add_argument("--octaves", type=int, default=None, help="default 4 (6 with --shard-image)")
     ap.add_argument("--scales", type=int, default=5)
     ap.add_argument("--skip-gauss-planes", action="store_true",
                     help="keypoints-only mode: do not materialise the Gaussian planes")
@@ -157,9 +157,18 @@ def main():
                          "octave0 / gaussian / refinement = own streams, image k+1 starts once image k has "
                          "passed that point (sift_order_after: software pipelining); full = own streams, "
                          "no ordering.  Per-kernel durations (roofline.achieved) include any overlap")
+    ap.add_argument("--shard-image", action="store_true",
+                    help="BASELINE cfg 5: ONE image per step split over all ranks in row bands (sift_amd.shard."
+                         "detect_sharded_device: band octaves, all-gathered next-octave base, tail octaves one per "
+                         "rank, block-major merge); strong scaling.  Defaults to 7680x4320, 6 octaves x 5 scales "
+                         "unless --width/--height/--octaves are given")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
     args = ap.parse_args()
+    big = args.shard_image
+    args.width = args.width or (7680 if big else 3840)
+    args.height = args.height or (4320 if big else 2160)
+    args.octaves = args.octaves or (6 if big else 4)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -181,6 +190,8 @@ def main():
         dist.init_process_group("nccl")  # RCCL over xGMI
     dev = local_rank
     W, H, O, S = args.width, args.height, args.octaves, args.scales
+    if args.shard_image:
+        return bench_shard_image(args, dist, world, rank, dev)
     flags = sift_amd.F_SKIP_GAUSS_PLANES if args.skip_gauss_planes else 0
     params = sift_amd.make_params(O, S, flags=flags)
 
@@ -399,6 +410,75 @@ def main():
         print(json.dumps(out), flush=True)
     for c in reversed(ctxs):
         c.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+def bench_shard_image(args, dist, world, rank, dev):
+    """BASELINE cfg 5: one image per step, row bands over the ranks (strong
+    scaling): value = input pixels of one image / time per image."""
+    import torch
+    import sift_amd
+    from sift_amd import shard
+    from sift_amd.synth import blob_image
+    W, H, O, S = args.width, args.height, args.octaves, args.scales
+    params = sift_amd.make_params(O, S)
+    img = blob_image(W, H, seed=42)
+    d_img = torch.from_numpy(img).to("cuda:%d" % dev)
+    ctx = sift_amd.Context(dev)
+    run = (lambda tm=None: shard.detect_sharded_device(ctx, d_img, params, timer=tm)) if dist is not None else \
+        (lambda tm=None: shard.detect_sharded_device_local(ctx, d_img, params, 1, timer=tm))
+    for _ in range(max(1, args.warmup)):
+        out, plan = run()
+    n_kp = int(out.shape[0])
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    parts = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, plan = run(parts)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    K = args.steps
+    if rank == 0:
+        out = {
+            "metric": metric_name(W, H, O, S) + " (one image split over the GPUs)",
+            "value": round(W * H / (elapsed / K) / 1e6, 3),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": "one %dx%d gray f32 image per step split over %d GPU%s in row bands (BASELINE cfg 5), "
+                            "%d octaves x %d scales, Gaussian+DoG+extrema+refine, whole-image keypoints on every "
+                            "rank" % (W, H, world, "s" if world > 1 else "", O, S),
+                "width": W, "height": H, "octaves": O, "scales_per_octave": S,
+                "parallelism": "row bands: octaves 0..%d on overlapping crops, octave-%d base all-gathered, tail "
+                               "octaves one per rank, counts + keypoints all-gathered, block-major merge"
+                               % (plan.K, plan.K + 1) if world > 1 else "single GPU (one band)",
+                "bands": plan.bands, "K": plan.K,
+            },
+            "parts_ms_per_step": {k: round(v / K * 1e3, 4) for k, v in parts.items()},
+            "keypoints": n_kp,
+            "roofline": None,
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
     return 0

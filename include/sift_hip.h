@@ -268,6 +268,21 @@ void *sift_stream(struct sift_ctx *ctx);
  * stay whole). */
 int sift_set_row_origin(struct sift_ctx *ctx, int input_row0);
 
+/* Keep only the keypoints whose candidate lies in input rows [row_begin,
+ * row_end) of the whole image (row_end < 0: to the bottom; row_begin < 0:
+ * every keypoint, the default) in the following refinements / detections
+ * (ABI version >= 5): a row band's share of a sharded image, decided by the
+ * candidate's octave row as the band plan cuts it (octave 0: 2 r, octave o:
+ * r >> (o - 1)).  Applied in the keypoint compaction on the device. */
+int sift_set_owned_rows(struct sift_ctx *ctx, int row_begin, int row_end);
+
+/* Kept keypoints per (octave, scale) block of the last refinement /
+ * detection (ABI version >= 5): counts[o * S + s - 1], *n_blocks =
+ * num_octaves * scales_per_octave.  Host memory; the keypoint list is in
+ * block order, so these are its block boundaries
+ * (sift_merge_keypoint_blocks_device). */
+int sift_last_block_counts(struct sift_ctx *ctx, int64_t *counts, int cap, int *n_blocks);
+
 /* The fp64 base of octave num_octaves formed by the last build with
  * SIFT_F_EXPORT_NEXT_SEED: rows x cols, row-major (host copy / device
  * pointer valid until the next build). */
@@ -283,6 +298,26 @@ int sift_detect_from_seed(struct sift_ctx *ctx, int octave_first, const double *
 int sift_detect_from_seed_device(struct sift_ctx *ctx, int octave_first, const double *d_seed, int width,
                                  int height, const sift_params *p, sift_keypoint *out, size_t cap,
                                  size_t *n_out);
+
+/* Detection of a tail of octaves split over several devices (ABI version >= 5):
+ * like sift_detect_from_seed_device, building octaves octave_first ..
+ * p->num_octaves - 1 from the fp64 base of octave_first, but scanning only
+ * octaves octave_scan_first .. p->num_octaves - 1 for extrema (the octaves
+ * before it are built for their seeds only).  Rank j of a row-band run builds
+ * the tail up to its octave and detects that one octave. */
+int sift_detect_from_seed_range_device(struct sift_ctx *ctx, int octave_first, int octave_scan_first,
+                                       const double *d_seed, int width, int height, const sift_params *p,
+                                       sift_keypoint *out, size_t cap, size_t *n_out);
+
+/* Block-major merge of keypoint lists in device memory (ABI version >= 5):
+ * d_in holds n_parts lists back to back; list q holds, in block order,
+ * counts[q * n_blocks + b] keypoints of block b.  d_out receives block 0 of
+ * every list in list order, then block 1, ...  With blocks = (octave, scale)
+ * and lists = row bands in row order, this is the reference's candidate order
+ * (octave, scale, y, x) without a sort.  counts is host memory; completes
+ * before return. */
+int sift_merge_keypoint_blocks_device(struct sift_ctx *ctx, const sift_keypoint *d_in, const int64_t *counts,
+                                      int n_parts, int n_blocks, sift_keypoint *d_out);
 
 /* The candidate (octave, scale, y, x) of each keypoint of the last
  * detection/refinement run with SIFT_F_KEYPOINT_ORIGINS: 4 int32 per

@@ -48,6 +48,11 @@ double js_round(double x) {
 
 enum DogSource { kNone = 0, kNative = 1, kForeign = 2 };
 
+// Device counter slots: 0..31 extrema / refinement counts (see below), then
+// the kept keypoints per (octave, scale) block from kBlk on.
+constexpr int kBlk = 64;
+constexpr int kCntAll = kBlk + kMaxOctaves * kMaxScales;
+
 }  // namespace
 
 struct sift_ctx {
@@ -81,6 +86,7 @@ struct sift_ctx {
   bool detect_host_img = false;
   ExtremaLaunch xl{};       // extrema launch state between prepare / scan / finish
   int o_first = 0;          // first octave of the pyramid in use (sift_detect_from_seed: > 0)
+  int scan_first = 0;       // first octave the extrema stage scans (>= o_first; sift_detect_from_seed_range)
   int row0 = 0;             // sift_set_row_origin: input row of the image's first row
   int xseed_h = 0, xseed_w = 0;  // SIFT_F_EXPORT_NEXT_SEED: the base of octave O
   bool has_xseed = false;
@@ -93,15 +99,19 @@ struct sift_ctx {
   // device memory
   DBuf img, seeds, gauss, dog, wts;
   DBuf base0;                                  // materialised octave-0 base (large radii only)
+  DBuf l64;                                    // fp64 Gaussian planes of the large-radius octaves
   std::vector<double> wts_host;                // taps last uploaded to wts
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
   DBuf keep, pos;                              // keypoint compaction
   DBuf status, kp_tmp, kp, uncertain;          // refinement
   DBuf xseed, kp_key;                          // next-octave base, keypoint origins
+  DBuf merge_tab;                              // sift_merge_keypoint_blocks_device tables
   DBuf counters, temp;
   DBuf rgba, alpha, display, mm_parts;         // image products (sift_image.hip)
-  unsigned* h_counters = nullptr;              // pinned mirror of counters
+  unsigned* h_counters = nullptr;              // pinned mirror of counters (+ per-block keypoint counts at kBlk)
+  int own_lo = -1, own_hi = -1;                // sift_set_owned_rows
+  std::vector<long long> blk_counts;           // kept keypoints per (octave, scale) of the last refinement
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
   hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
@@ -194,8 +204,8 @@ static int ctx_create(int device, sift_ctx* share, sift_ctx** out) {
   if (hipSetDevice(device) != hipSuccess ||
       (share ? (ctx->stream = share->stream, false)
              : hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) ||
-      hipHostMalloc((void**)&ctx->h_counters, 64 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
-      ctx->counters.ensure(64 * sizeof(unsigned)) != hipSuccess) {
+      hipHostMalloc((void**)&ctx->h_counters, kCntAll * sizeof(unsigned), hipHostMallocDefault) != hipSuccess ||
+      ctx->counters.ensure(kCntAll * sizeof(unsigned)) != hipSuccess) {
     delete ctx;
     return SIFT_E_HIP;
   }
@@ -242,11 +252,11 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
+  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->l64, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->xseed, &ctx->kp_key, &ctx->counters,
-                  &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts};
+                  &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -325,6 +335,7 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
     goff += NS * plane;
     doff += ND * plane;
     oc.rmax = 0;
+    oc.l64_off = -1;
     for (int s = 0; s < NS; ++s) {
       const double sg = ctx->sigma[o * NS + s];
       int r = 0;
@@ -408,6 +419,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   Pyramid& P = ctx->P;
   if (o_first < 0 || o_first >= P.O) return set_err(ctx, SIFT_E_ARG, "octave_first out of range");
   ctx->o_first = o_first;
+  ctx->scan_first = o_first;
   ctx->has_xseed = false;
   const long long tot = total_plane_px(ctx);
   const bool keep_gauss = !(p->flags & SIFT_F_SKIP_GAUSS_PLANES);
@@ -435,6 +447,16 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   }
   P.seeds = ctx->seeds.as<double>();
   P.dog = ctx->dog.as<float>();
+  {  // large-radius octaves keep their fp64 Gaussian planes (the exact passes read them)
+    long long l64 = 0;
+    for (int o = o_first; o < P.O; ++o)
+      if (gauss_keep_l64(P, o)) {
+        P.oct[o].l64_off = l64;
+        l64 += (long long)P.NS * P.oct[o].h * P.oct[o].w;
+      }
+    if (l64) HIPCHK(ctx->l64.ensure((size_t)l64 * sizeof(double)));
+    P.l64 = l64 ? ctx->l64.as<double>() : nullptr;
+  }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   const double* base0 = nullptr;
   if (o_first == 0 && gauss_needs_base0(P)) {
@@ -493,6 +515,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
       HIPCHK(hipStreamWaitEvent(ctx->hi, ctx->ev_hi_fork, 0));
       ls = ctx->hi;
     }
+    L.l64 = P.oct[o].l64_off >= 0 ? ctx->l64.as<double>() + P.oct[o].l64_off : nullptr;
     HIPCHK(launch_gauss_dog(P, L, ls));
     if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ls));
     HIPCHK(hipEventRecord(ctx->ev_go[o], ls));
@@ -799,7 +822,7 @@ static int extrema_finish(sift_ctx* ctx) {
 // The whole extrema stage on the context stream.
 static int launch_extrema_stage(sift_ctx* ctx) {
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  int o0 = ctx->o_first;
+  int o0 = std::max(ctx->o_first, ctx->scan_first);
   if (ctx->x_prepared) {  // octaves < x_nf were decided in the Gaussian pass
     ctx->x_prepared = false;
     o0 = std::max(o0, ctx->x_nf);
@@ -862,6 +885,7 @@ static int refine_enqueue(sift_ctx* ctx) {
     HIPCHK(hipMemsetAsync(cnt + kCntKp, 0, sizeof(unsigned), ctx->stream));
     HIPCHK(hipMemsetAsync(cnt + 16, 0, 16 * sizeof(unsigned), ctx->stream));
   }
+  HIPCHK(hipMemsetAsync(cnt + kBlk, 0, (kCntAll - kBlk) * sizeof(unsigned), ctx->stream));
   ctx->counters_zeroed = false;
   ctx->n_kp = 0;
   ctx->n_sing = 0;
@@ -883,7 +907,8 @@ static int refine_enqueue(sift_ctx* ctx) {
     HIPCHK(hipEventRecord(ctx->ev_heavy, ctx->stream));  // the rest is latency-bound tail work
     // Uncertain decisions exist only with fp32-rounded native planes.
     if (ctx->dog_source == kNative) HIPCHK(launch_refine_exact(P, R, ctx->stream));
-    HIPCHK(launch_status_to_keep(R.status, ctx->keep.as<unsigned>(), R.n, cap, ctx->stream));
+    HIPCHK(launch_status_to_keep(P, R.status, R.cand_key, ctx->keep.as<unsigned>(), R.n, cap, ctx->own_lo,
+                                 ctx->own_hi, cnt + kBlk, ctx->stream));
     size_t tb = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), cap,
                                             ctx->stream));
@@ -891,17 +916,17 @@ static int refine_enqueue(sift_ctx* ctx) {
     tb = ctx->temp.bytes;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), cap,
                                             ctx->stream));
-    HIPCHK(launch_scatter_keypoints(R.status, ctx->pos.as<unsigned>(), R.kp, R.n, cap, ctx->kp.as<Keypoint>(),
-                                    ctx->stream));
+    HIPCHK(launch_scatter_keypoints(ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), R.kp, R.n, cap,
+                                    ctx->kp.as<Keypoint>(), ctx->stream));
     HIPCHK(launch_count_keypoints(ctx->pos.as<unsigned>(), ctx->keep.as<unsigned>(), R.n, cap, cnt + kCntKp, ctx->stream));
     if (ctx->p.flags & SIFT_F_KEYPOINT_ORIGINS) {
       HIPCHK(ctx->kp_key.ensure((size_t)cap * sizeof(unsigned)));
-      HIPCHK(launch_scatter_keys(R.status, ctx->pos.as<unsigned>(), R.cand_key, R.n, cap, ctx->kp_key.as<unsigned>(),
-                                 ctx->stream));
+      HIPCHK(launch_scatter_keys(ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), R.cand_key, R.n, cap,
+                                 ctx->kp_key.as<unsigned>(), ctx->stream));
     }
   }
   ctx->has_origins = (ctx->p.flags & SIFT_F_KEYPOINT_ORIGINS) != 0;
-  HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, 32 * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, kCntAll * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->stream));
   return SIFT_OK;
 }
@@ -922,6 +947,9 @@ static int refine_settle(sift_ctx* ctx) {
   ctx->n_exact += h[kCntUnc];
   ctx->n_kp = cap > 0 ? h[kCntKp] : 0;
   ctx->n_sing = h[kCntSing];
+  ctx->blk_counts.assign((size_t)ctx->P.O * ctx->P.S, 0);
+  if (cap > 0)
+    for (size_t b = 0; b < ctx->blk_counts.size(); ++b) ctx->blk_counts[b] = h[kBlk + b];
   if (std::getenv("SIFT_DEBUG_REFINE"))
     std::fprintf(stderr,
                  "refine uncertain %u: det %u alpha %u omega %u edge_dt %u edge_int %u round %u | iter %u %u %u %u %u"
@@ -1246,13 +1274,17 @@ int sift_next_seed(sift_ctx* ctx, double* dst, size_t cap, int* rows, int* cols)
 }
 
 static int detect_from_seed(sift_ctx* ctx, int o_first, const double* seed_host, const double* seed_dev, int W,
-                            int H, const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
+                            int H, const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out,
+                            int scan_first = 0) {
   if (!ctx || !p) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
   if (ctx->detect_pending) return set_err(ctx, SIFT_E_STATE, "a detection is in flight on this context");
   if (o_first < 1) return set_err(ctx, SIFT_E_ARG, "octave_first must be >= 1");
+  if (scan_first && (scan_first < o_first || scan_first >= p->num_octaves))
+    return set_err(ctx, SIFT_E_ARG, "octave_scan_first outside [octave_first, num_octaves)");
   int rc = build_common(ctx, nullptr, nullptr, W, H, 0, p, nullptr, false, o_first, seed_host, seed_dev);
   if (rc) return rc;
+  if (scan_first) ctx->scan_first = scan_first;
   rc = launch_extrema_stage(ctx);
   if (rc) return rc;
   rc = refine_enqueue(ctx);
@@ -1270,6 +1302,54 @@ int sift_detect_from_seed(sift_ctx* ctx, int octave_first, const double* seed, i
 int sift_detect_from_seed_device(sift_ctx* ctx, int octave_first, const double* d_seed, int width, int height,
                                  const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
   return detect_from_seed(ctx, octave_first, nullptr, d_seed, width, height, p, out, cap, n_out);
+}
+
+int sift_detect_from_seed_range_device(sift_ctx* ctx, int octave_first, int octave_scan_first, const double* d_seed,
+                                       int width, int height, const sift_params* p, sift_keypoint* out, size_t cap,
+                                       size_t* n_out) {
+  return detect_from_seed(ctx, octave_first, nullptr, d_seed, width, height, p, out, cap, n_out,
+                          std::max(octave_scan_first, octave_first));
+}
+
+int sift_merge_keypoint_blocks_device(sift_ctx* ctx, const sift_keypoint* d_in, const int64_t* counts, int n_parts,
+                                      int n_blocks, sift_keypoint* d_out) {
+  if (!ctx || !counts || n_parts < 1 || n_blocks < 1 || n_parts > 1024 || n_blocks > 4096) return SIFT_E_ARG;
+  // tab: part_start[np + 1] | in_start[np][nb + 1] | out_off[nb][np]
+  const int np = n_parts, nb = n_blocks;
+  std::vector<long long> tab((size_t)(np + 1) + (size_t)np * (nb + 1) + (size_t)nb * np);
+  long long* part_start = tab.data();
+  long long* in_start = part_start + np + 1;
+  long long* out_off = in_start + (size_t)np * (nb + 1);
+  long long n = 0;
+  for (int q = 0; q < np; ++q) {
+    part_start[q] = n;
+    long long a = 0;
+    for (int b = 0; b < nb; ++b) {
+      const long long c = counts[(size_t)q * nb + b];
+      if (c < 0) return set_err(ctx, SIFT_E_ARG, "negative count");
+      in_start[(size_t)q * (nb + 1) + b] = a;
+      a += c;
+    }
+    in_start[(size_t)q * (nb + 1) + nb] = a;
+    n += a;
+  }
+  part_start[np] = n;
+  long long o = 0;
+  for (int b = 0; b < nb; ++b)
+    for (int q = 0; q < np; ++q) {
+      out_off[(size_t)b * np + q] = o;
+      o += counts[(size_t)q * nb + b];
+    }
+  if (n == 0) return SIFT_OK;
+  if (!d_in || !d_out) return SIFT_E_ARG;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(ctx->merge_tab.ensure(tab.size() * sizeof(long long)));
+  HIPCHK(hipMemcpyAsync(ctx->merge_tab.p, tab.data(), tab.size() * sizeof(long long), hipMemcpyHostToDevice,
+                        ctx->stream));
+  HIPCHK(launch_merge_blocks(reinterpret_cast<const Keypoint*>(d_in), n, ctx->merge_tab.as<long long>(), np, nb,
+                             reinterpret_cast<Keypoint*>(d_out), ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return SIFT_OK;
 }
 
 int sift_order_after(sift_ctx* ctx, const sift_ctx* prev, int after) {
@@ -1390,6 +1470,28 @@ int sift_plane_image(sift_ctx* ctx, int kind, int octave, int scale, int mode, d
 int sift_plane_image_device(sift_ctx* ctx, int kind, int octave, int scale, int mode, double coefficient,
                             uint8_t* d_rgba, size_t cap_bytes) {
   return plane_image_common(ctx, kind, octave, scale, mode, coefficient, d_rgba, cap_bytes, false);
+}
+
+int sift_set_owned_rows(sift_ctx* ctx, int row_begin, int row_end) {
+  if (!ctx) return SIFT_E_ARG;
+  if (row_begin < 0) {
+    ctx->own_lo = ctx->own_hi = -1;
+    return SIFT_OK;
+  }
+  if (row_end >= 0 && row_end < row_begin) return set_err(ctx, SIFT_E_ARG, "row_end < row_begin");
+  ctx->own_lo = row_begin;
+  ctx->own_hi = row_end;
+  return SIFT_OK;
+}
+
+int sift_last_block_counts(sift_ctx* ctx, int64_t* counts, int cap, int* n_blocks) {
+  if (!ctx) return SIFT_E_ARG;
+  const int n = (int)ctx->blk_counts.size();
+  if (n_blocks) *n_blocks = n;
+  if (!counts) return SIFT_OK;
+  if (cap < n) return set_err(ctx, SIFT_E_CAPACITY, "destination too small (num_octaves * scales_per_octave)");
+  for (int b = 0; b < n; ++b) counts[b] = ctx->blk_counts[b];
+  return SIFT_OK;
 }
 
 int sift_set_row_origin(sift_ctx* ctx, int input_row0) {

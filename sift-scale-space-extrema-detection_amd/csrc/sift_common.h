@@ -30,6 +30,7 @@ struct Octave {
   int wofs[kMaxScales];  // offset of tap 0 of scale s in wts (PAD zeros precede it)
   int rad[kMaxScales];   // radius of scale s (0 = un-blurred copy)
   int rmax;
+  long long l64_off;     // element offset of plane (o, 0) in l64 (fp64 Gaussian planes), -1 = not kept
 };
 
 struct Pyramid {
@@ -39,6 +40,7 @@ struct Pyramid {
   const double* seeds;
   const double* wts;
   const float* dog;
+  const double* l64;     // fp64 Gaussian planes of the octaves built by the wide-radius path (l64_off >= 0)
   double pix_thr;        // 0.8 * thr   (sift.js:285-294)
   double thr;            // thr         (background.js:572)
   int row0;              // input row of the input's first row (a row-band crop; 0 = whole image)

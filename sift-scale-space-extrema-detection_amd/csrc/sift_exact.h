@@ -28,6 +28,16 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int o, int s, int y, int
   const Octave& oc = P.oct[o];
   const int h = oc.h, w = oc.w;
   const int lane = threadIdx.x & 63;
+  if (oc.l64_off >= 0) {  // the wide-radius path kept this octave's fp64 Gaussian planes: the values themselves
+    if (lane < 27) {
+      const int k = lane / 9, q = lane - 9 * k, a = q / 3, c = q - 3 * a;
+      const long long plane = (long long)h * w;
+      const double* L0 = P.l64 + oc.l64_off + (long long)(s - 1 + k) * plane + (long long)(y - 1 + a) * w + (x - 1 + c);
+      d27[lane] = L0[0] - L0[plane];
+    }
+    __syncthreads();
+    return;
+  }
   const int nc0 = 2 * oc.rad[s - 1] + 3, nc1 = 2 * oc.rad[s] + 3, nc2 = 2 * oc.rad[s + 1] + 3,
             nc3 = 2 * oc.rad[s + 2] + 3;
   const int o1 = 3 * nc0, o2 = o1 + 3 * nc1, o3 = o2 + 3 * nc2, o4 = o3 + 3 * nc3;

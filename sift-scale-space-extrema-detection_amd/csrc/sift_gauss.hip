@@ -670,6 +670,18 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
         }
       }
     }
+    if (L.l64 && s >= s_begin) {  // fp64 plane for the exact passes
+      double* lp = L.l64 + s * plane;
+#pragma unroll
+      for (int i = 0; i < kNR; ++i) {
+        const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
+        if (own[i]) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (q < nvalid) lp[(long long)y * T.w + x + q] = out[i][q];
+        }
+      }
+    }
     if (s == P.S && L.next_seed && s >= s_begin) {
 #pragma unroll
       for (int i = 0; i < kNR; ++i) {
@@ -713,6 +725,15 @@ __global__ __launch_bounds__(256) void k_dog_from_gauss(const float* __restrict_
 }
 
 bool gauss_needs_base0(const Pyramid& P) { return P.oct[0].rmax > kUR; }
+
+// Octaves o >= 1 whose largest radius reaches SIFT_L64_R (default 90; 0 =
+// never) also store their fp64 Gaussian planes: the exact passes read them
+// instead of recomputing 3x3x3 patches with 189- and 377-tap chains (8K O=6
+// S=5: octaves 4 and 5; at 4K octave 3, radius 47, it measured slower: 0.71 -> 0.74 ms pass).
+bool gauss_keep_l64(const Pyramid& P, int o) {
+  static const int rmin = [] { const char* e = std::getenv("SIFT_L64_R"); return e ? std::atoi(e) : 90; }();
+  return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin;
+}
 
 static bool staged0(const Pyramid& P, int o) { return o == 0 && !gauss_needs_base0(P); }
 

@@ -40,6 +40,7 @@ struct GaussLaunch {
   double* next_seed;  // base of octave o+1 (nullptr for the last octave)
   int next_w;
   const double* base; // fp64 octave base h x w (o >= 1: the seed; o == 0: only when materialised)
+  double* l64;        // plane (o, 0) of the kept fp64 Gaussian planes, nullptr = not kept
   // filled by launch_gauss_dog
   int sw;             // strip row stride (doubles)
   int vec;            // float4 plane stores are aligned
@@ -132,6 +133,10 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st);
 inline int fused_words_per_row(int w) { return w > 2 ? (w - 2 + kFX - 1) / kFX : 1; }
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
 
+// Octave o stores its fp64 Gaussian planes too (GaussLaunch.l64): the exact
+// passes then read the patch values instead of recomputing them.
+bool gauss_keep_l64(const Pyramid& P, int o);
+
 // Fills the unit table of L (octave geometry) and launches the scan; returns
 // the launch error.  L.bitmap words per octave: S * h * nw.
 hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, int o_begin, int o_end);
@@ -146,17 +151,26 @@ hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, hipStrea
 
 // Order-preserving compaction helpers.
 // Entries i >= *n (device count) of the cap-sized arrays are inactive.
-hipError_t launch_scatter_keypoints(const int* status, const unsigned* pos, const Keypoint* kp,
+hipError_t launch_scatter_keypoints(const unsigned* keep, const unsigned* pos, const Keypoint* kp,
                                     const unsigned* n, int cap, Keypoint* out, hipStream_t st);
-hipError_t launch_status_to_keep(const int* status, unsigned* keep, const unsigned* n, int cap,
-                                 hipStream_t st);
-hipError_t launch_scatter_keys(const int* status, const unsigned* pos, const unsigned* key, const unsigned* n,
+// keep[i] = status[i] is a kept keypoint whose candidate row (whole-image
+// octave rows, P.row0 applied) lies in the input rows [own_lo, own_hi) (own_lo
+// < 0: every row; own_hi < 0: no upper bound); blk[o * S + s - 1] counts them
+// per (octave, scale).
+hipError_t launch_status_to_keep(const Pyramid& P, const int* status, const unsigned* key, unsigned* keep,
+                                 const unsigned* n, int cap, int own_lo, int own_hi, unsigned* blk, hipStream_t st);
+hipError_t launch_scatter_keys(const unsigned* keep, const unsigned* pos, const unsigned* key, const unsigned* n,
                                int cap, unsigned* out, hipStream_t st);
 // out = pos[n-1] + keep[n-1] (0 if n == 0): the number of keypoints.
 hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, const unsigned* n, int cap,
                                   unsigned* out, hipStream_t st);
 
 size_t exact_lds_bytes(const Pyramid& P);
+
+// Block-major merge of n keypoints in np parts (sift_merge_keypoint_blocks_device):
+// tab = part_start[np + 1] | in_start[np][nb + 1] | out_off[nb][np] (device).
+hipError_t launch_merge_blocks(const Keypoint* in, long long n, const long long* tab, int np, int nb, Keypoint* out,
+                               hipStream_t st);
 
 // keys -> 4 int32 per keypoint: octave, scale, whole-image octave row (row0 applied), x.
 hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st);

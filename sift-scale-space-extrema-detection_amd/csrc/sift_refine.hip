@@ -423,31 +423,59 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
   }
 }
 
-__global__ __launch_bounds__(256) void k_status_to_keep(const int* __restrict__ status,
-                                                        unsigned* __restrict__ keep,
-                                                        const unsigned* __restrict__ n, int cap) {
+__global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const int* __restrict__ status,
+                                                        const unsigned* __restrict__ key,
+                                                        unsigned* __restrict__ keep, const unsigned* __restrict__ n,
+                                                        int cap, int own_lo, int own_hi,
+                                                        unsigned* __restrict__ blk) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < cap) keep[i] = (i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep) ? 1u : 0u;
+  int b = -1;  // (octave, scale) block of a kept keypoint
+  if (i < cap) {
+    bool k = i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep;
+    if (k) {
+      int o, s, y, x;
+      decode_key(P, key[i], o, s, y, x);
+      if (own_lo >= 0) {  // row-band ownership by candidate row (octave o rows: 2 r at o = 0, r >> (o-1))
+        const int yw = y + ((P.row0 * 2) >> o);
+        const int lo = o == 0 ? 2 * own_lo : own_lo >> (o - 1);
+        const int hi = own_hi < 0 ? 0x7fffffff : (o == 0 ? 2 * own_hi : own_hi >> (o - 1));
+        k = yw >= lo && yw < hi;
+      }
+      if (k) b = o * P.S + (s - 1);
+    }
+    keep[i] = k ? 1u : 0u;
+  }
+  // per-block counts, one atomic per distinct block of the wave (keys are sorted)
+  for (;;) {
+    const unsigned long long act = __ballot(b >= 0);
+    if (!act) break;
+    const int lead = __ffsll((long long)act) - 1;
+    const int first = __shfl(b, lead);
+    const unsigned long long same = __ballot(b == first);
+    if ((int)(threadIdx.x & 63) == lead) atomicAdd(&blk[first], (unsigned)__popcll(same));
+    if (b == first) b = -1;
+  }
 }
 
-__global__ __launch_bounds__(256) void k_scatter_kp(const int* __restrict__ status,
+// keep: k_status_to_keep's flags (kept keypoint, in the owned rows).
+__global__ __launch_bounds__(256) void k_scatter_kp(const unsigned* __restrict__ keep,
                                                     const unsigned* __restrict__ pos,
                                                     const Keypoint* __restrict__ kp,
                                                     const unsigned* __restrict__ n, int cap,
                                                     Keypoint* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < cap && i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep) out[pos[i]] = kp[i];
+  if (i < cap && i < (int)min(*n, (unsigned)cap) && keep[i]) out[pos[i]] = kp[i];
 }
 
 // Candidate key of every kept keypoint, in keypoint order (the origin of a
 // keypoint for callers that merge partial results, e.g. row-band shards).
-__global__ __launch_bounds__(256) void k_scatter_key(const int* __restrict__ status,
+__global__ __launch_bounds__(256) void k_scatter_key(const unsigned* __restrict__ keep,
                                                      const unsigned* __restrict__ pos,
                                                      const unsigned* __restrict__ key,
                                                      const unsigned* __restrict__ n, int cap,
                                                      unsigned* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < cap && i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep) out[pos[i]] = key[i];
+  if (i < cap && i < (int)min(*n, (unsigned)cap) && keep[i]) out[pos[i]] = key[i];
 }
 
 __global__ void k_count_kp(const unsigned* __restrict__ pos, const unsigned* __restrict__ keep,
@@ -467,6 +495,35 @@ __global__ __launch_bounds__(256) void k_decode_origins(const Pyramid P, const u
   out[4 * i + 1] = s;
   out[4 * i + 2] = y + ((P.row0 * 2) >> o);
   out[4 * i + 3] = x;
+}
+
+// One thread per keypoint: its part (linear, np small), its block (binary
+// search of the part's block starts), its place in the block-major output.
+__global__ __launch_bounds__(256) void k_merge_blocks(const Keypoint* __restrict__ in, long long n,
+                                                      const long long* __restrict__ tab, int np, int nb,
+                                                      Keypoint* __restrict__ out) {
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= n) return;
+  const long long* part_start = tab;
+  const long long* in_start = tab + np + 1;
+  const long long* out_off = in_start + (long long)np * (nb + 1);
+  int p = 0;
+  while (p + 1 < np && i >= part_start[p + 1]) ++p;
+  const long long local = i - part_start[p];
+  const long long* st = in_start + (long long)p * (nb + 1);
+  int lo = 0, hi = nb - 1;  // largest b with st[b] <= local (empty blocks: st[b] == st[b+1])
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (st[mid] <= local) lo = mid; else hi = mid - 1;
+  }
+  out[out_off[(long long)lo * np + p] + (local - st[lo])] = in[i];
+}
+
+hipError_t launch_merge_blocks(const Keypoint* in, long long n, const long long* tab, int np, int nb, Keypoint* out,
+                               hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, tab, np, nb, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st) {
@@ -489,24 +546,25 @@ hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, hipStrea
   return hipGetLastError();
 }
 
-hipError_t launch_status_to_keep(const int* status, unsigned* keep, const unsigned* n, int cap,
-                                 hipStream_t st) {
+hipError_t launch_status_to_keep(const Pyramid& P, const int* status, const unsigned* key, unsigned* keep,
+                                 const unsigned* n, int cap, int own_lo, int own_hi, unsigned* blk, hipStream_t st) {
   if (cap <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_status_to_keep, dim3((cap + 255) / 256), dim3(256), 0, st, status, keep, n, cap);
+  hipLaunchKernelGGL(k_status_to_keep, dim3((cap + 255) / 256), dim3(256), 0, st, P, status, key, keep, n, cap,
+                     own_lo, own_hi, blk);
   return hipGetLastError();
 }
 
-hipError_t launch_scatter_keypoints(const int* status, const unsigned* pos, const Keypoint* kp,
+hipError_t launch_scatter_keypoints(const unsigned* keep, const unsigned* pos, const Keypoint* kp,
                                     const unsigned* n, int cap, Keypoint* out, hipStream_t st) {
   if (cap <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter_kp, dim3((cap + 255) / 256), dim3(256), 0, st, status, pos, kp, n, cap, out);
+  hipLaunchKernelGGL(k_scatter_kp, dim3((cap + 255) / 256), dim3(256), 0, st, keep, pos, kp, n, cap, out);
   return hipGetLastError();
 }
 
-hipError_t launch_scatter_keys(const int* status, const unsigned* pos, const unsigned* key, const unsigned* n,
+hipError_t launch_scatter_keys(const unsigned* keep, const unsigned* pos, const unsigned* key, const unsigned* n,
                                int cap, unsigned* out, hipStream_t st) {
   if (cap <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter_key, dim3((cap + 255) / 256), dim3(256), 0, st, status, pos, key, n, cap, out);
+  hipLaunchKernelGGL(k_scatter_key, dim3((cap + 255) / 256), dim3(256), 0, st, keep, pos, key, n, cap, out);
   return hipGetLastError();
 }
 

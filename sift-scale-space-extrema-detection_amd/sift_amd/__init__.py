@@ -54,6 +54,8 @@ ABI_SYMBOLS = (
     "sift_rgba_to_gray", "sift_rgba_to_gray_device", "sift_build_scale_space_rgba", "sift_detect_rgba",
     "sift_plane_image", "sift_plane_image_device", "sift_detect_begin_async", "sift_detect_end_async",
     "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device", "sift_last_octave_timings",
+    "sift_detect_from_seed_range_device", "sift_merge_keypoint_blocks_device", "sift_set_owned_rows",
+    "sift_last_block_counts",
 )
 
 
@@ -153,6 +155,12 @@ def lib():
         "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
         "sift_last_timings": (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
         "sift_last_octave_timings": (ctypes.c_int, [vp, dp, ctypes.c_int, ip]),
+        "sift_detect_from_seed_range_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int,
+                                                              ctypes.c_int, pp, vp, sz, szp]),
+        "sift_merge_keypoint_blocks_device": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
+                                                             ctypes.c_int, vp]),
+        "sift_set_owned_rows": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
+        "sift_last_block_counts": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ip]),
         "sift_device_keypoints": (ctypes.c_int, [vp, ctypes.POINTER(vp), szp]),
         "sift_stream": (vp, [vp]),
         "sift_synchronize": (ctypes.c_int, [vp]),
@@ -492,6 +500,44 @@ class Context:
         self._check(rc, "sift_detect_from_seed_device")
         self.params, self.width, self.height = params, width, height
         return n.value
+
+    def detect_from_seed_range_device(self, d_seed, octave_first, octave_scan_first, width, height, params,
+                                      raise_singular=False):
+        """Build octaves octave_first.. from the device fp64 base, detect only
+        octaves octave_scan_first..params.num_octaves-1 (keypoints stay on
+        device; returns the count)."""
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect_from_seed_range_device(self._h, int(octave_first), int(octave_scan_first),
+                                                        ctypes.c_void_p(int(d_seed)), int(width), int(height),
+                                                        ctypes.byref(params), None, 0, ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect_from_seed_range_device")
+        self.params, self.width, self.height = params, width, height
+        return n.value
+
+    def merge_keypoint_blocks_device(self, d_in, counts, d_out):
+        """Block-major merge of keypoint lists on the device; counts: int64
+        (n_parts, n_blocks) host array."""
+        c = np.ascontiguousarray(counts, dtype=np.int64)
+        self._check(self._L.sift_merge_keypoint_blocks_device(self._h, ctypes.c_void_p(int(d_in)),
+                                                              c.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                              c.shape[0], c.shape[1], ctypes.c_void_p(int(d_out))),
+                    "sift_merge_keypoint_blocks_device")
+
+    def set_owned_rows(self, row_begin, row_end=-1):
+        """Keep only keypoints whose candidate lies in input rows [row_begin,
+        row_end) (row_end < 0: to the bottom; row_begin < 0: all)."""
+        self._check(self._L.sift_set_owned_rows(self._h, int(row_begin), int(row_end)), "sift_set_owned_rows")
+
+    def block_counts(self):
+        """Kept keypoints per (octave, scale) of the last refinement: int64 [O * S]."""
+        n = ctypes.c_int()
+        self._check(self._L.sift_last_block_counts(self._h, None, 0, ctypes.byref(n)), "sift_last_block_counts")
+        out = np.zeros(max(n.value, 1), dtype=np.int64)
+        self._check(self._L.sift_last_block_counts(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                   out.shape[0], ctypes.byref(n)), "sift_last_block_counts")
+        return out[:n.value]
 
     def set_row_origin(self, input_row0):
         """Input row of the first row of the following images (a row-band crop)."""

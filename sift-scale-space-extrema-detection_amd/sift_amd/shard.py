@@ -289,12 +289,21 @@ def torch_ready(t):
         torch.cuda.current_stream(t.device).synchronize()
 
 
+def _device_keypoints(ctx, n, torch, dev):
+    kp = torch.empty((max(n, 1), REC), dtype=torch.uint8, device=dev)
+    if n:
+        ctx.copy_keypoints_device(kp.data_ptr(), n)
+    return kp[:n]
+
+
 def run_shard_device(ctx, d_img, params, plan, r):
     """Shard r from the whole image `d_img` (H x W fp32 torch tensor on ctx's
-    device): (keypoints uint8 [n, 48], origins int32 [n, 4], owned base rows
-    fp64 [rows, cols] or None), all on the device.  The sift_* copies into
-    the returned tensors complete before they return, so torch may read them
-    at once."""
+    device): (keypoints uint8 [n, 48] on the device -- only those whose
+    candidate row the shard owns, filtered in the library's compaction
+    (sift_set_owned_rows) --, their counts per (octave, scale) block (int64
+    numpy [K+1 octaves * S]), owned rows of the octave-(K+1) base fp64
+    [rows, cols] on the device or None).  The sift_* copies into the returned
+    tensors complete before they return, so torch may read them at once."""
     import torch
     dev = d_img.device
     torch_ready(d_img)
@@ -303,13 +312,15 @@ def run_shard_device(ctx, d_img, params, plan, r):
     K = plan.K
     last = r == len(plan.bands) - 1
     W = plan.width
-    flags = params.flags | F_KEYPOINT_ORIGINS | (F_EXPORT_NEXT_SEED if plan.has_tail else 0)
+    flags = params.flags | (F_EXPORT_NEXT_SEED if plan.has_tail else 0)
     p = make_params(K + 1, params.scales_per_octave, params.min_blur, params.assumed_blur,
                     params.min_interpixel_distance, flags)
     ctx.set_row_origin(c0)
+    ctx.set_owned_rows(lo, -1 if last else hi)
     try:
         n = ctx.detect_device(d_img.data_ptr() + c0 * W * 4, W, c1 - c0, p)
-        kp, org = _device_lists(ctx, n, torch, dev)
+        kp = _device_keypoints(ctx, n, torch, dev)
+        counts = ctx.block_counts()
         part = None
         if plan.has_tail:
             s0, s1 = _seed_rows(plan, r)
@@ -318,14 +329,8 @@ def run_shard_device(ctx, d_img, params, plan, r):
             ctx.copy_next_seed_device(part.data_ptr(), part.numel(), s0, s1)
     finally:
         ctx.set_row_origin(0)
-    o = org[:, 0].long()
-    y = org[:, 2].long()
-    lo_o = torch.where(o == 0, torch.full_like(o, 2 * lo), lo >> (o - 1).clamp(min=0))
-    keep = y >= lo_o
-    if not last:
-        hi_o = torch.where(o == 0, torch.full_like(o, 2 * hi), hi >> (o - 1).clamp(min=0))
-        keep &= y < hi_o
-    return kp[keep], org[keep], part
+        ctx.set_owned_rows(-1)
+    return kp, counts, part
 
 
 def run_tail_device(ctx, d_base, params, plan):
@@ -342,16 +347,58 @@ def run_tail_device(ctx, d_base, params, plan):
     return _device_lists(ctx, n, torch, d_base.device)
 
 
-def merge_device(kps, orgs):
-    """Ordered merge on the device: one argsort of the 48-bit candidate key
-    (octave, scale, y, x).  (A sort-free merge -- per (octave, scale) block
-    offsets from bincounts and prefix sums, one scatter -- measured slower at
-    8K, 1.02-1.08 vs 0.89 ms: a dozen small torch ops and a host sync.)"""
+def tail_octaves(plan, world):
+    """Tail octave -> rank: the trailing octaves K+1..O-1 are detected one per
+    rank; each rank builds the tail's Gaussian chain only as far as its octave
+    (sift_detect_from_seed_range_device), so the deepest octave is the
+    longest piece.  The deepest go to the ranks with the smallest crops (the
+    first and last bands carry a margin on one side only)."""
+    if not plan.has_tail:
+        return {}
+    n = len(plan.crops)
+    ranks = sorted(range(min(world, n)), key=lambda r: (plan.crops[r][1] - plan.crops[r][0], r))
+    tail = list(range(plan.num_octaves - 1, plan.K, -1))
+    return {t: ranks[i % len(ranks)] for i, t in enumerate(tail)}
+
+
+def run_tail_octave_device(ctx, d_base, params, plan, t):
+    """Keypoints of tail octave t alone (uint8 [n, 48] on the device) and
+    their block counts, from the gathered octave-(K+1) base: octaves K+1..t
+    are built, only t is scanned (sift_detect_from_seed_range_device)."""
     import torch
-    kp = torch.cat(kps)
-    org = torch.cat(orgs).long()
-    key = ((org[:, 0] * 16 + org[:, 1]) * (1 << 20) + org[:, 2]) * (1 << 20) + org[:, 3]
-    return kp[torch.argsort(key)]
+    p = make_params(t + 1, params.scales_per_octave, params.min_blur, params.assumed_blur,
+                    params.min_interpixel_distance, params.flags)
+    h, w = octave_dims(plan.width, plan.height, plan.num_octaves)[plan.K + 1]
+    if tuple(d_base.shape) != (h, w):
+        raise ValueError("gathered base %s != octave %d dims %s" % (tuple(d_base.shape), plan.K + 1, (h, w)))
+    d_base = d_base.contiguous()
+    torch_ready(d_base)  # the all-gather / concatenation that made it is only enqueued on torch's stream
+    n = ctx.detect_from_seed_range_device(d_base.data_ptr(), plan.K + 1, t, plan.width, plan.height, p)
+    return _device_keypoints(ctx, n, torch, d_base.device), ctx.block_counts()
+
+
+def _blocks(counts, O, S):
+    """Block counts of a part padded to all O * S blocks (a band or tail part
+    covers only its leading octaves)."""
+    out = np.zeros(O * S, dtype=np.int64)
+    out[:len(counts)] = counts
+    return out
+
+
+def merge_device(ctx, kps, counts, O, S):
+    """Ordered merge without a sort: parts are row bands in row order (plus
+    tail octaves), each sorted by candidate (octave, scale, y, x), so the
+    reference's order is block-major over (octave, scale), then part order
+    (sift_merge_keypoint_blocks_device).  counts: per part, its keypoints per
+    block (host)."""
+    import torch
+    kp = torch.cat(kps).contiguous() if len(kps) > 1 else kps[0].contiguous()
+    out = torch.empty_like(kp)
+    if kp.shape[0]:
+        torch_ready(kp)
+        ctx.merge_keypoint_blocks_device(kp.data_ptr(), np.stack([_blocks(c, O, S) for c in counts]),
+                                         out.data_ptr())
+    return out
 
 
 def _sync(t):
@@ -362,29 +409,35 @@ def _sync(t):
 
 def detect_sharded_device_local(ctx, d_img, params, n_shards, max_overhead=0.5, timer=None):
     """All shards on one device in turn (device-resident): the sharded
-    algorithm without the collectives.  Returns (uint8 [n, 48] keypoints on
-    the device, plan).  timer: optional dict of per-part seconds."""
+    algorithm without the collectives -- one rank's band after another, then
+    every tail octave as its own piece, then the block merge.  Returns (uint8
+    [n, 48] keypoints on the device, plan).  timer: optional dict of per-part
+    seconds (each part synchronised, so the parts can be summed into a
+    modelled critical path)."""
     import torch
     H, W = d_img.shape
+    O, S = params.num_octaves, params.scales_per_octave
     plan = plan_bands(W, H, params, n_shards, max_overhead)
-    kps, orgs, seeds = [], [], []
+    kps, counts, seeds = [], [], []
     for r in range(len(plan.bands)):
         t0 = time.perf_counter()
-        kp, org, seed = run_shard_device(ctx, d_img, params, plan, r)
+        kp, cnt, seed = run_shard_device(ctx, d_img, params, plan, r)
         _sync(d_img)
         _tick(timer, "shard%d" % r, t0)
         kps.append(kp)
-        orgs.append(org)
+        counts.append(cnt)
         seeds.append(seed)
     if plan.has_tail:
-        t0 = time.perf_counter()
-        kp, org = run_tail_device(ctx, torch.cat(seeds), params, plan)
-        _sync(d_img)
-        _tick(timer, "tail", t0)
-        kps.append(kp)
-        orgs.append(org)
+        base = torch.cat(seeds)
+        for t in tail_octaves(plan, len(plan.bands)):
+            t0 = time.perf_counter()
+            kp, cnt = run_tail_octave_device(ctx, base, params, plan, t)
+            _sync(d_img)
+            _tick(timer, "tail%d" % t, t0)
+            kps.append(kp)
+            counts.append(cnt)
     t0 = time.perf_counter()
-    out = merge_device(kps, orgs)
+    out = merge_device(ctx, kps, counts, O, S)
     _sync(d_img)
     _tick(timer, "merge", t0)
     return out, plan
@@ -405,37 +458,59 @@ def gather_rows(t, counts, group=None):
     return torch.cat([recv[i * m:i * m + counts[i]] for i in range(world)])
 
 
-def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5):
-    """One shard per rank, device-resident (RCCL with the nccl backend):
-    gather the owned base rows (the tail runs on rank 0), then the keypoints
-    and their origins; every rank returns the whole image's keypoints
-    (uint8 [n, 48] on its device) in the reference's order."""
+def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, timer=None):
+    """One shard per rank, device-resident (RCCL with the nccl backend).
+    Rank r runs its row band (octaves 0..K, keypoints of its own rows), the
+    owned rows of the octave-(K+1) base are all-gathered, tail octave K+1+j is
+    detected by rank j (round robin), then the per-(octave, scale) counts and
+    the keypoints are all-gathered and merged block-major (no sort).  Every
+    rank returns the whole image's keypoints (uint8 [n, 48] on its device) in
+    the reference's order."""
     import torch
     import torch.distributed as dist
     H, W = d_img.shape
+    O, S = params.num_octaves, params.scales_per_octave
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = d_img.device
     plan = plan_bands(W, H, params, world, max_overhead)
     nb = len(plan.bands)
+    t0 = time.perf_counter()
     if rank < nb:
-        kp, org, seed = run_shard_device(ctx, d_img, params, plan, rank)
+        kp, cnt, seed = run_shard_device(ctx, d_img, params, plan, rank)
     else:
-        kp = torch.zeros((0, REC), dtype=torch.uint8, device=dev)
-        org = torch.zeros((0, 4), dtype=torch.int32, device=dev)
-        seed = None
+        kp, cnt, seed = torch.zeros((0, REC), dtype=torch.uint8, device=dev), np.zeros(0, np.int64), None
+    t0 = _tick(timer, "band", t0)
+    kps, cnts = [kp], [_blocks(cnt, O, S)]
     if plan.has_tail:
         cols = octave_dims(W, H, plan.num_octaves)[plan.K + 1][1]
         rows = [(lambda a: a[1] - a[0])(_seed_rows(plan, r)) if r < nb else 0 for r in range(world)]
         mine = seed if seed is not None else torch.zeros((0, cols), dtype=torch.float64, device=dev)
         base = gather_rows(mine, rows, group)
-        if rank == 0:
-            tk, to = run_tail_device(ctx, base, params, plan)
-            kp, org = torch.cat([kp, tk]), torch.cat([org, to])
-    cnt = torch.tensor([kp.shape[0]], dtype=torch.int64, device=dev)
-    cnts = torch.zeros(world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(cnts, cnt, group=group)
-    counts = [int(c) for c in cnts.tolist()]
-    all_kp = gather_rows(kp, counts, group)
-    all_org = gather_rows(org, counts, group)
-    return merge_device([all_kp], [all_org]), plan
+        t0 = _tick(timer, "base_gather", t0)
+        for t, owner in tail_octaves(plan, world).items():
+            if owner == rank:
+                tk, tc = run_tail_octave_device(ctx, base, params, plan, t)
+                kps.append(tk)
+                cnts.append(_blocks(tc, O, S))
+        t0 = _tick(timer, "tail", t0)
+    kp = torch.cat(kps)
+    mine_cnt = torch.from_numpy(np.sum(cnts, axis=0).astype(np.int64)).to(dev)
+    all_cnt = torch.zeros(world * O * S, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(all_cnt, mine_cnt, group=group)
+    counts = all_cnt.view(world, O * S).cpu().numpy()
+    all_kp = gather_rows(kp, [int(c) for c in counts.sum(axis=1)], group)
+    t0 = _tick(timer, "kp_gather", t0)
+    out = _merge_gathered(ctx, all_kp, counts, O, S)
+    _tick(timer, "merge", t0)
+    return out, plan
+
+
+def _merge_gathered(ctx, all_kp, counts, O, S):
+    """Merge of the rank-order concatenation of every rank's block-ordered list."""
+    import torch
+    out = torch.empty_like(all_kp)
+    if all_kp.shape[0]:
+        torch_ready(all_kp)
+        ctx.merge_keypoint_blocks_device(all_kp.data_ptr(), counts, out.data_ptr())
+    return out

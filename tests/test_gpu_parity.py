@@ -370,3 +370,27 @@ def test_keypoint_origins_and_next_seed(gpu_ctx):
     p4 = sift_amd.make_params(4, 3)
     gpu_ctx.build_scale_space(img, p4)
     np.testing.assert_array_equal(seed.astype(np.float32), gpu_ctx.plane(sift_amd.PLANE_GAUSS, 3, 0))
+
+
+def test_owned_rows_and_block_counts(gpu_ctx):
+    """sift_set_owned_rows keeps exactly the keypoints whose candidate row lies
+    in the band (octave rows 2 r at octave 0, r >> (o-1) above); the per-block
+    counts are the list's (octave, scale) boundaries."""
+    from sift_amd.shard import _owned
+    img = blob_image(400, 300, seed=17)
+    O, S = 4, 4
+    p = sift_amd.make_params(O, S, flags=sift_amd.F_KEYPOINT_ORIGINS)
+    whole = gpu_ctx.detect(img, p).copy()
+    org = gpu_ctx.keypoint_origins()
+    blk = gpu_ctx.block_counts()
+    np.testing.assert_array_equal(blk, np.bincount(org[:, 0] * S + org[:, 1] - 1, minlength=O * S))
+    for lo, hi in ((0, 96), (96, 200), (200, -1)):
+        gpu_ctx.set_owned_rows(lo, hi)
+        try:
+            kp = gpu_ctx.detect(img, p).copy()
+            counts = gpu_ctx.block_counts()
+        finally:
+            gpu_ctx.set_owned_rows(-1)
+        keep = _owned(org, lo, hi, hi < 0)
+        assert kp.tobytes() == whole[keep].tobytes()
+        np.testing.assert_array_equal(counts, np.bincount(org[keep, 0] * S + org[keep, 1] - 1, minlength=O * S))

@@ -162,10 +162,26 @@ def test_merge_orders_by_candidate():
 class FakeDeviceCtx(FakeCtx):
     """The device-resident interface of sift_amd.Context over CPU tensors:
     'device pointers' are host addresses of CPU tensors (ctypes.memmove)."""
+    own = (-1, -1)
+
+    def set_owned_rows(self, lo, hi=-1):
+        self.own = (lo, hi)
+
+    def _blocks(self, p):
+        o, s = self.org[self.last, 0], self.org[self.last, 1]
+        return np.bincount(o * p.scales_per_octave + s - 1,
+                           minlength=p.num_octaves * p.scales_per_octave).astype(np.int64)
 
     def detect_device(self, ptr, W, h, p):
         self.detect(np.zeros((h, W), np.float32), p)
+        lo, hi = self.own
+        if lo >= 0:
+            self.last &= _owned(self.org, lo, hi, hi < 0)
+        self.blk = self._blocks(p)
         return int(self.last.sum())
+
+    def block_counts(self):
+        return self.blk
 
     def copy_keypoints_device(self, ptr, cap):
         import ctypes
@@ -194,6 +210,28 @@ class FakeDeviceCtx(FakeCtx):
         base = np.frombuffer((ctypes.c_double * (h * w)).from_address(ptr), dtype=np.float64).reshape(h, w)
         self.detect_from_seed(base.copy(), o_first, W, H, p)
         return int(self.last.sum())
+
+    def detect_from_seed_range_device(self, ptr, o_first, o_scan, W, H, p):
+        self.detect_from_seed_device(ptr, o_first, W, H, p)
+        o = self.org[:, 0]
+        self.last = (o >= o_scan) & (o < p.num_octaves)
+        self.blk = self._blocks(p)
+        return int(self.last.sum())
+
+    def merge_keypoint_blocks_device(self, d_in, counts, d_out):
+        import ctypes
+        counts = np.asarray(counts, dtype=np.int64)
+        n = int(counts.sum())
+        buf = np.frombuffer(ctypes.string_at(d_in, n * 48), dtype=np.uint8).reshape(n, 48)
+        parts, off = [], 0
+        for q in range(counts.shape[0]):
+            blocks = []
+            for b in range(counts.shape[1]):
+                blocks.append(buf[off:off + counts[q, b]])
+                off += counts[q, b]
+            parts.append(blocks)
+        out = np.concatenate([parts[q][b] for b in range(counts.shape[1]) for q in range(counts.shape[0])])
+        ctypes.memmove(d_out, out.tobytes(), out.nbytes)
 
 
 @pytest.mark.parametrize("shape,n", [((480, 360, 4, 3), 3), ((7680, 4320, 6, 5), 8), ((640, 600, 5, 3), 1)])
@@ -244,11 +282,13 @@ def test_detect_sharded_device_gathers_world2(shape):
 
 
 def test_merge_device_equals_sort():
-    """The sort-free device merge equals a full sort by candidate on ragged
-    parts that own disjoint row ranges per (octave, scale), plus a tail."""
+    """The sort-free block-major device merge (sift_merge_keypoint_blocks_device,
+    stand-in context) equals a full sort by candidate on ragged parts that own
+    disjoint row ranges per (octave, scale), plus tail octaves."""
     import torch
     from sift_amd.shard import merge_device
     kp, org = _fake_truth(640, 600, 5, n=300, seed=4)
+    ctx = FakeDeviceCtx(640, 600, 5)
     # split octaves 0..2 into 3 row bands, octaves 3..4 = tail
     parts = []
     for lo, hi in ((0, 100), (100, 250), (250, 10 ** 6)):
@@ -259,5 +299,6 @@ def test_merge_device_equals_sort():
     orgs = [torch.from_numpy(org[m].copy()) for m in parts]
     kps.insert(1, kps[0][:0])
     orgs.insert(1, orgs[0][:0])
-    out = merge_device(kps, orgs)
+    counts = [np.bincount(o[:, 0].numpy() * 3 + o[:, 1].numpy() - 1, minlength=15) for o in orgs]
+    out = merge_device(ctx, kps, counts, 5, 3)
     assert out.numpy().tobytes() == kp.tobytes()

@@ -2,8 +2,9 @@
 """cfg 5 (8K, O=6, S=5) on one GPU, device-resident: whole-image detection
 (input in HBM, keypoints left in HBM) vs the same image as n row-band shards
 run in turn through sift_amd.shard.detect_sharded_device_local, with per-part
-times -- the critical path n devices would see is the slowest shard + the
-tail + the merge (plus two all-gathers, not timed here).
+times -- the critical path n devices would see is the slowest rank (its band
++ the tail octave it detects) + the merge (plus two all-gathers, not timed
+here).
 usage: tools/shard_time_device.py [n_shards] [reps]"""
 import json
 import os
@@ -44,12 +45,20 @@ for _ in range(reps):
 keys = timers[0].keys()
 med = {k: float(np.median([t[k] for t in timers])) * 1e3 for k in keys}
 shards = [med["shard%d" % r] for r in range(len(plan.bands))]
-crit = max(shards) + med.get("tail", 0.0) + med["merge"]
+tails = {t: med["tail%d" % t] for t in shard.tail_octaves(plan, len(plan.bands))}
+owner = shard.tail_octaves(plan, len(plan.bands))
+per_rank = [shards[r] + sum(v for t, v in tails.items() if owner[t] == r) for r in range(len(plan.bands))]
+crit = max(per_rank) + med["merge"]
 print(json.dumps({"config": "8K 7680x4320 O6 S5, device-resident (image in HBM, keypoints in HBM)",
                   "n_shards": n, "K": plan.K, "bands": plan.bands, "crops": plan.crops,
                   "whole_ms": round(1e3 * float(np.median(t_whole)), 3),
                   "shard_ms": [round(x, 3) for x in shards],
-                  "tail_ms": round(med.get("tail", 0.0), 3), "merge_ms": round(med["merge"], 3),
+                  "tail_octave_ms": {str(t): round(v, 3) for t, v in tails.items()},
+                  "tail_owner": {str(t): r for t, r in owner.items()},
+                  "per_rank_ms": [round(x, 3) for x in per_rank],
+                  "merge_ms": round(med["merge"], 3),
                   "critical_path_ms": round(crit, 3),
+                  "critical_path_note": "slowest rank (its band + the tail octave it detects) + the block merge; "
+                                        "the two all-gathers (octave-(K+1) base rows, keypoints) are not in it",
                   "speedup_vs_whole": round(1e3 * float(np.median(t_whole)) / crit, 2),
                   "keypoints": n_whole, "identical": bool(same)}))
