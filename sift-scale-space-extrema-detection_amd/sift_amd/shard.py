@@ -429,7 +429,7 @@ def detect_sharded_device_local(ctx, d_img, params, n_shards, max_overhead=0.5, 
         seeds.append(seed)
     if plan.has_tail:
         base = torch.cat(seeds)
-        for t in tail_octaves(plan, len(plan.bands)):
+        for t in sorted(tail_octaves(plan, len(plan.bands))):
             t0 = time.perf_counter()
             kp, cnt = run_tail_octave_device(ctx, base, params, plan, t)
             _sync(d_img)
@@ -488,7 +488,7 @@ def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, time
         mine = seed if seed is not None else torch.zeros((0, cols), dtype=torch.float64, device=dev)
         base = gather_rows(mine, rows, group)
         t0 = _tick(timer, "base_gather", t0)
-        for t, owner in tail_octaves(plan, world).items():
+        for t, owner in sorted(tail_octaves(plan, world).items()):  # a rank's list stays in block order
             if owner == rank:
                 tk, tc = run_tail_octave_device(ctx, base, params, plan, t)
                 kps.append(tk)
