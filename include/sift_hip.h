@@ -58,9 +58,10 @@ enum {
   SIFT_F_SKIP_DOG_PLANES = 1 << 1,   /* reserved: DoG planes are needed by refinement today   */
   SIFT_F_EXPORT_NEXT_SEED = 1 << 2,  /* also form the fp64 base of octave num_octaves (sift_next_seed) */
   SIFT_F_KEYPOINT_ORIGINS = 1 << 3,  /* record each keypoint's candidate (sift_keypoint_origins) */
-  SIFT_F_FUSED_EXTREMA = 1 << 4      /* detections: decide octave 0's extrema inside its Gaussian+DoG
+  SIFT_F_FUSED_EXTREMA = 1 << 4,     /* detections: decide octave 0's extrema inside its Gaussian+DoG
                                         pass instead of re-reading its DoG planes (same results;
                                         measured slower on MI355X) */
+  SIFT_F_LOW_CONTRAST_LIST = 1 << 5  /* also list the low-contrast extrema (sift_copy_low_contrast) */
 };
 
 /* Parameters of the pipeline.  Names and defaults follow
@@ -168,6 +169,18 @@ int sift_load_scale_space(struct sift_ctx *ctx, const float *planes, int width, 
  * SIFT_E_CAPACITY: *n_out = required count, nothing written. */
 int sift_find_extrema(struct sift_ctx *ctx, sift_extremum *out, size_t cap, size_t *n_out,
                       size_t *n_low_contrast);
+
+/* The low-contrast extrema of the last extrema stage run with
+ * SIFT_F_LOW_CONTRAST_LIST in its parameters (ABI version >= 5): strict
+ * 26-neighbour extrema with |v| < 0.8*thr, the reference's
+ * lowContrastKeypoints (sift.js:293-306), in its order (octave, scale, y, x)
+ * with their DoG values.  SIFT_E_CAPACITY: *n_out = required count. */
+int sift_copy_low_contrast(struct sift_ctx *ctx, sift_extremum *out, size_t cap, size_t *n_out);
+
+/* Replace the sift_params.flags the context's current pyramid was built or
+ * loaded with, for the stages that follow (ABI version >= 5): e.g.
+ * SIFT_F_LOW_CONTRAST_LIST before sift_find_extrema on a built pyramid. */
+int sift_set_flags(struct sift_ctx *ctx, int flags);
 
 /* refineCandidateKeypoints (background.js:455-685) on the candidates of the
  * last sift_find_extrema (or sift_set_candidates).  Output keeps reference

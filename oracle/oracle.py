@@ -99,6 +99,33 @@ def split_pyramid(flat, dims, per_octave):
     return out
 
 
+def extrema_lists(p, W, H, dog_flat):
+    """Candidate and low-contrast extrema of a flat fp64 DoG pyramid (any
+    source: computed here or the fp32 planes a caller loads), reference order:
+    ((rec (N,4) int32, value (N,)), (low_rec, low_value))."""
+    L = lib()
+    dog_flat = np.ascontiguousarray(dog_flat, dtype=np.float64)
+    low = ctypes.c_long(0)
+    dogp = _ptr(dog_flat, ctypes.c_double)
+    n = L.oracle_find_extrema_ex(ctypes.byref(p), W, H, dogp, None, None, 0, None, None, 0, ctypes.byref(low))
+    nl = int(low.value)
+    rec = np.zeros((max(n, 1), 4), dtype=np.int32)
+    val = np.zeros(max(n, 1))
+    low_rec = np.zeros((max(nl, 1), 4), dtype=np.int32)
+    low_val = np.zeros(max(nl, 1))
+    L.oracle_find_extrema_ex(ctypes.byref(p), W, H, dogp, _ptr(rec, ctypes.c_int32), _ptr(val, ctypes.c_double), n,
+                             _ptr(low_rec, ctypes.c_int32), _ptr(low_val, ctypes.c_double), nl, ctypes.byref(low))
+    return (rec[:n], val[:n]), (low_rec[:nl], low_val[:nl])
+
+
+def as_records(rec, val):
+    """(N,5) [octave, scale, x, y, value] rows of an extrema list."""
+    c = np.zeros((rec.shape[0], 5))
+    c[:, :4] = rec
+    c[:, 4] = val
+    return c
+
+
 class OracleRun:
     """Full oracle pipeline on one image; keeps flat fp64 pyramids."""
 
@@ -126,31 +153,15 @@ class OracleRun:
                 self.gauss = split_pyramid(self.gauss_flat, self.dims, S + 3)
             del gauss_flat
             self.dog = split_pyramid(self.dog_flat, self.dims, S + 2)
-            low = ctypes.c_long(0)
-            dogp = _ptr(self.dog_flat, ctypes.c_double)
-            n = L.oracle_find_extrema_ex(ctypes.byref(p), W, H, dogp, None, None, 0, None, None, 0,
-                                         ctypes.byref(low))
-            nl = int(low.value)
-            self.cand_rec = np.zeros((max(n, 1), 4), dtype=np.int32)
-            self.cand_val = np.zeros(max(n, 1))
-            self.low_rec = np.zeros((max(nl, 1), 4), dtype=np.int32)
-            self.low_val = np.zeros(max(nl, 1))
-            L.oracle_find_extrema_ex(ctypes.byref(p), W, H, dogp, _ptr(self.cand_rec, ctypes.c_int32),
-                                     _ptr(self.cand_val, ctypes.c_double), n, _ptr(self.low_rec, ctypes.c_int32),
-                                     _ptr(self.low_val, ctypes.c_double), nl, ctypes.byref(low))
+            (self.cand_rec, self.cand_val), (self.low_rec, self.low_val) = extrema_lists(p, W, H, self.dog_flat)
         finally:
             set_threads(1)
-        self.cand_rec, self.cand_val = self.cand_rec[:n], self.cand_val[:n]
-        self.low_rec, self.low_val = self.low_rec[:nl], self.low_val[:nl]
-        self.n_low = nl
+        self.n_low = self.low_rec.shape[0]
         self.refined, self.n_singular = self.refine(self.cand_rec, self.cand_val)
 
     def low_contrast(self):
         """(N,5) [octave, scale, x, y, value] of the low-contrast extrema, reference order."""
-        c = np.zeros((self.low_rec.shape[0], 5))
-        c[:, :4] = self.low_rec
-        c[:, 4] = self.low_val
-        return c
+        return as_records(self.low_rec, self.low_val)
 
     def refine(self, rec, val):
         rec = np.ascontiguousarray(rec, dtype=np.int32)
@@ -166,10 +177,7 @@ class OracleRun:
 
     def candidates(self):
         """(N,5) [octave, scale, x, y, value] in reference order."""
-        c = np.zeros((self.cand_rec.shape[0], 5))
-        c[:, :4] = self.cand_rec
-        c[:, 4] = self.cand_val
-        return c
+        return as_records(self.cand_rec, self.cand_val)
 
 
 def detect_count(img, p, mode=CONV_2D):

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -74,6 +75,10 @@ struct sift_ctx {
   bool have_cand = false;
   size_t n_cand = 0, n_low = 0, n_kp = 0, n_sing = 0, n_exact = 0;
   size_t n_slots = 0;       // candidate slots (n_cand + entries dropped by the exact pass)
+  bool want_low = false;    // this extrema stage lists the low-contrast extrema
+  bool have_low = false;    // the last extrema stage did (sift_copy_low_contrast)
+  unsigned low_cap = 0;     // slots of the ordered low-contrast list
+  size_t n_low_sure = 0, n_low_late = 0;  // ordered (certain) and exact-pass (late) low-contrast entries
   unsigned cand_cap = 0;    // capacity of the candidate slot arrays (extrema path)
   unsigned amb_cap = 0;     // capacity of the ambiguous-key list
   int slot_cap = 0;         // slots the refinement runs over
@@ -103,6 +108,8 @@ struct sift_ctx {
   std::vector<double> wts_host;                // taps last uploaded to wts
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
+  DBuf lowbitmap, lowrowcount, lowrowoff;      // low-contrast list (SIFT_F_LOW_CONTRAST_LIST)
+  DBuf low_key, low_val, late_key, late_val;
   DBuf keep, pos;                              // keypoint compaction
   DBuf status, kp_tmp, kp, uncertain;          // refinement
   DBuf xseed, kp_key;                          // next-octave base, keypoint origins
@@ -256,7 +263,9 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->xseed, &ctx->kp_key, &ctx->counters,
-                  &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab};
+                  &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab,
+                  &ctx->lowbitmap, &ctx->lowrowcount, &ctx->lowrowoff, &ctx->low_key, &ctx->low_val,
+                  &ctx->late_key, &ctx->late_val};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -467,7 +476,8 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   ctx->scans_done = false;
   ctx->x_prepared = false;
   const bool overlap = overlap_extrema && ctx->side;
-  const int nf = (fuse_extrema && !overlap && o_first == 0 && fuse_enabled(p) && gauss_can_fuse(P, 0)) ? 1 : 0;
+  const int nf = (fuse_extrema && !overlap && o_first == 0 && fuse_enabled(p) && gauss_can_fuse(P, 0) &&
+                  !(p->flags & SIFT_F_LOW_CONTRAST_LIST)) ? 1 : 0;
   if (nf) {  // bitmap geometry, counter resets: before the fused launch writes them
     ctx->dog_source = kNative;
     rc = extrema_prepare(ctx, ctx->stream, nf);
@@ -692,7 +702,8 @@ static float round_toward(double v, int dir) {
 // Counter slots (ctx->counters): [0] ambiguous keys, [1] low-contrast
 // extrema, [2] slots dropped by the exact pass, [3] uncertain refinements,
 // [4] singular Hessians, [12] candidate slots, [13] keypoints, [16..] debug.
-enum { kCntAmb = 0, kCntLow = 1, kCntDrop = 2, kCntUnc = 3, kCntSing = 4, kCntN = 12, kCntKp = 13 };
+enum { kCntAmb = 0, kCntLow = 1, kCntDrop = 2, kCntUnc = 3, kCntSing = 4, kCntLowLate = 6, kCntLowSure = 7,
+       kCntN = 12, kCntKp = 13 };
 constexpr int kRetry = 1;  // internal: a capacity overflowed, grow and run again
 
 // The extrema stage, launched without waiting, in three parts:
@@ -741,6 +752,19 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   HIPCHK(ctx->cand_key.ensure((size_t)ctx->cand_cap * sizeof(unsigned)));
   HIPCHK(ctx->cand_val.ensure((size_t)ctx->cand_cap * sizeof(double)));
   HIPCHK(ctx->cand_keep.ensure((size_t)ctx->cand_cap * sizeof(unsigned)));
+  ctx->want_low = (ctx->p.flags & SIFT_F_LOW_CONTRAST_LIST) != 0;
+  ctx->have_low = false;
+  if (ctx->want_low) {
+    ctx->low_cap = std::max(ctx->low_cap, std::max(65536u, ctx->cand_cap / 4));
+    HIPCHK(ctx->lowbitmap.ensure((size_t)words * sizeof(unsigned long long)));
+    HIPCHK(ctx->lowrowcount.ensure((size_t)(rows + 1) * sizeof(unsigned)));
+    HIPCHK(ctx->lowrowoff.ensure((size_t)(rows + 1) * sizeof(unsigned)));
+    HIPCHK(ctx->low_key.ensure((size_t)ctx->low_cap * sizeof(unsigned)));
+    HIPCHK(ctx->low_val.ensure((size_t)ctx->low_cap * sizeof(double)));
+    HIPCHK(ctx->late_key.ensure((size_t)ctx->amb_cap * sizeof(unsigned)));
+    HIPCHK(ctx->late_val.ensure((size_t)ctx->amb_cap * sizeof(double)));
+    HIPCHK(hipMemsetAsync(ctx->lowrowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), st));
+  }
   // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
   // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
   const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
@@ -761,6 +785,8 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   L.amb_keys = ctx->amb_keys.as<unsigned>();
   L.counters = cnt;
   L.amb_cap = ctx->amb_cap;
+  L.lowbitmap = ctx->want_low ? ctx->lowbitmap.as<unsigned long long>() : nullptr;
+  L.lowrowcount = ctx->want_low ? ctx->lowrowcount.as<unsigned>() : nullptr;
   return SIFT_OK;
 }
 
@@ -802,7 +828,38 @@ static int extrema_finish(sift_ctx* ctx) {
     E.cap = ctx->cand_cap;
     HIPCHK(launch_emit(P, E, ctx->stream));
   }
+  if (ctx->want_low) {  // the certain low-contrast extrema, in order (same scan + emission as the candidates)
+    size_t lb = 0;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, lb, ctx->lowrowcount.as<unsigned>(),
+                                            ctx->lowrowoff.as<unsigned>(), (int)(rows + 1), ctx->stream));
+    HIPCHK(ctx->temp.ensure(lb));
+    lb = ctx->temp.bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, lb, ctx->lowrowcount.as<unsigned>(),
+                                            ctx->lowrowoff.as<unsigned>(), (int)(rows + 1), ctx->stream));
+    HIPCHK(hipMemcpyAsync(cnt + kCntLowSure, ctx->lowrowoff.as<unsigned>() + rows, sizeof(unsigned),
+                          hipMemcpyDeviceToDevice, ctx->stream));
+    EmitLaunch E{};
+    E.n_oct = P.O;
+    for (int o = 0; o < P.O; ++o) {
+      E.row_off[o] = (int)ctx->x_row_off[o];
+      E.word_off[o] = ctx->x_word_off[o];
+      E.nw[o] = ctx->x_nw[o];
+      E.ww[o] = ctx->x_ww[o];
+      E.woff[o] = ctx->x_woff[o];
+    }
+    E.row_off[P.O] = (int)rows;
+    E.bitmap = ctx->lowbitmap.as<unsigned long long>();
+    E.rowcount = ctx->lowrowcount.as<unsigned>();
+    E.rowoff = ctx->lowrowoff.as<unsigned>();
+    E.keys = ctx->low_key.as<unsigned>();
+    E.value = ctx->low_val.as<double>();
+    E.keep = nullptr;
+    E.cap = ctx->low_cap;
+    HIPCHK(launch_emit(P, E, ctx->stream));
+  }
   ExactLaunch X{};
+  X.late_keys = ctx->want_low ? ctx->late_key.as<unsigned>() : nullptr;
+  X.late_vals = ctx->want_low ? ctx->late_val.as<double>() : nullptr;
   X.amb_keys = ctx->amb_keys.as<unsigned>();
   X.amb_cap = ctx->amb_cap;
   X.keys = ctx->cand_key.as<unsigned>();
@@ -841,11 +898,16 @@ static int settle_extrema(sift_ctx* ctx) {
   const unsigned* h = ctx->h_counters;
   ctx->ext_pending = false;
   const unsigned n = h[kCntN], n_amb = h[kCntAmb];
-  if (n > ctx->cand_cap || n_amb > ctx->amb_cap) {
+  const unsigned n_ls = ctx->want_low ? h[kCntLowSure] : 0u;
+  if (n > ctx->cand_cap || n_amb > ctx->amb_cap || n_ls > ctx->low_cap) {
     if (n > ctx->cand_cap) ctx->cand_cap = n + n / 4 + 1024;
     if (n_amb > ctx->amb_cap) ctx->amb_cap = n_amb + n_amb / 4 + 1024;
+    if (n_ls > ctx->low_cap) ctx->low_cap = n_ls + n_ls / 4 + 1024;
     return kRetry;
   }
+  ctx->have_low = ctx->want_low;
+  ctx->n_low_sure = n_ls;
+  ctx->n_low_late = ctx->want_low ? h[kCntLowLate] : 0u;
   ctx->n_exact = n_amb;
   ctx->n_low = h[kCntLow];
   ctx->n_slots = n;
@@ -1008,6 +1070,48 @@ int sift_copy_candidates(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* 
     ++j;
   }
   if (n_out) *n_out = j;
+  return SIFT_OK;
+}
+
+int sift_copy_low_contrast(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (!ctx->have_low) return set_err(ctx, SIFT_E_STATE, "no low-contrast list (SIFT_F_LOW_CONTRAST_LIST)");
+  const size_t ns = ctx->n_low_sure, nl = ctx->n_low_late, n = ns + nl;
+  if (n_out) *n_out = n;
+  if (!out) return SIFT_OK;
+  if (cap < n) return set_err(ctx, SIFT_E_CAPACITY, "low-contrast buffer too small");
+  std::vector<unsigned> k(n);
+  std::vector<double> v(n);
+  if (n) {
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ns) {
+      HIPCHK(hipMemcpyAsync(k.data(), ctx->low_key.p, ns * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipMemcpyAsync(v.data(), ctx->low_val.p, ns * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (nl) {
+      HIPCHK(hipMemcpyAsync(k.data() + ns, ctx->late_key.p, nl * sizeof(unsigned), hipMemcpyDeviceToHost,
+                            ctx->stream));
+      HIPCHK(hipMemcpyAsync(v.data() + ns, ctx->late_val.p, nl * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  // The late entries (exact-pass decisions, unordered) merge into the ordered list by key.
+  std::vector<size_t> idx(n);
+  for (size_t i = 0; i < n; ++i) idx[i] = i;
+  std::sort(idx.begin() + ns, idx.end(), [&](size_t a, size_t b) { return k[a] < k[b]; });
+  std::inplace_merge(idx.begin(), idx.begin() + ns, idx.end(), [&](size_t a, size_t b) { return k[a] < k[b]; });
+  const Pyramid& P = ctx->P;
+  for (size_t j = 0; j < n; ++j) {
+    const unsigned key = k[idx[j]];
+    int o = 0;
+    while (o + 1 < P.O && key >= P.oct[o + 1].key_off) ++o;
+    const unsigned plane = (unsigned)P.oct[o].h * (unsigned)P.oct[o].w, r = key - P.oct[o].key_off;
+    out[j].octave = o;
+    out[j].scale = (int)(r / plane) + 1;
+    out[j].y = (int)((r % plane) / (unsigned)P.oct[o].w);
+    out[j].x = (int)((r % plane) % (unsigned)P.oct[o].w);
+    out[j].value = v[idx[j]];
+  }
   return SIFT_OK;
 }
 
@@ -1470,6 +1574,12 @@ int sift_plane_image(sift_ctx* ctx, int kind, int octave, int scale, int mode, d
 int sift_plane_image_device(sift_ctx* ctx, int kind, int octave, int scale, int mode, double coefficient,
                             uint8_t* d_rgba, size_t cap_bytes) {
   return plane_image_common(ctx, kind, octave, scale, mode, coefficient, d_rgba, cap_bytes, false);
+}
+
+int sift_set_flags(sift_ctx* ctx, int flags) {
+  if (!ctx) return SIFT_E_ARG;
+  ctx->p.flags = flags;
+  return SIFT_OK;
 }
 
 int sift_set_owned_rows(sift_ctx* ctx, int row_begin, int row_end) {

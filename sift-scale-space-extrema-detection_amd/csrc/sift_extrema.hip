@@ -47,6 +47,8 @@ struct XUnit {
   unsigned key_base;   // key of (s_first, 0, 0)
   unsigned long long* bitmap;  // (s_first, row 0, word 0) of this octave
   unsigned* rowcount;          // (s_first, row 0) of this octave
+  unsigned long long* lowbitmap;  // the same for the certain low-contrast extrema (LOWL)
+  unsigned* lowrowcount;
   unsigned low;
 };
 
@@ -62,7 +64,7 @@ __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int
 }
 
 // Centre row y (slots A = y-1, B = y, C = y+1): decide every scale of the group.
-template <int NP, int A, int B, int C>
+template <int NP, int A, int B, int C, bool LOWL>
 __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const ExtremaLaunch& L, int y) {
 #if defined(SIFT_X_PROBE)  // timing probe: no decisions
   {
@@ -80,6 +82,7 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     vn[q] = min3f(Wn.hn[A][q], Wn.hn[B][q], Wn.hn[C][q]);
   }
   unsigned wlo = 0, whi = 0, wcnt = 0;
+  unsigned llo = 0, lhi = 0, lcnt = 0;  // LOWL: the low-contrast word
 #pragma unroll
   for (int q = 1; q <= NP - 2; ++q) {
     const float v = Wn.cv[B][q];
@@ -87,14 +90,23 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     const float nmin = min3f(vn[q - 1], vn[q + 1], min3f(Wn.hn[A][q], Wn.hn[C][q], Wn.en[B][q]));
     const unsigned key = U.key_base + (unsigned)(q - 1) * (unsigned)U.plane + (unsigned)y * (unsigned)U.w +
                          (unsigned)(U.xw * kXW - 1 + U.lane);
+    unsigned long long lowmask;
     const unsigned long long bit = x_row_decide(v, nmax, nmin, U.colmask, L.c_lo, L.c_hi, L.exact_planes != 0, key,
-                                                &L.counters[0], L.amb_keys, L.amb_cap, U.low);
+                                                &L.counters[0], L.amb_keys, L.amb_cap, U.low, lowmask);
     if (bit) {
       const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
       if (U.lane == q - 1) {
         wlo = (unsigned)word;
         whi = (unsigned)(word >> 32);
         wcnt = (unsigned)__popcll(word);
+      }
+    }
+    if (LOWL && lowmask) {
+      const unsigned long long word = lowmask >> 1;
+      if (U.lane == q - 1) {
+        llo = (unsigned)word;
+        lhi = (unsigned)(word >> 32);
+        lcnt = (unsigned)__popcll(word);
       }
     }
   }
@@ -106,10 +118,14 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     const long long r = (long long)U.lane * U.h + y;
     U.bitmap[r * U.nw + U.xw] = ((unsigned long long)whi << 32) | wlo;
     if (wcnt) atomicAdd(&U.rowcount[r], wcnt);
+    if (LOWL) {
+      U.lowbitmap[r * U.nw + U.xw] = ((unsigned long long)lhi << 32) | llo;
+      if (lcnt) atomicAdd(&U.lowrowcount[r], lcnt);
+    }
   }
 }
 
-template <int NP>
+template <int NP, bool LOWL>
 __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int o, int s_first, int xw,
                                        int y0, int y1) {
   const Octave& oc = P.oct[o];
@@ -132,6 +148,10 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   U.key_base = oc.key_off + (unsigned)(s_first - 1) * (unsigned)U.plane;
   U.bitmap = L.bitmap + L.word_off[o] + (long long)(s_first - 1) * oc.h * U.nw;
   U.rowcount = L.rowcount + L.row_off[o] + (s_first - 1) * oc.h;
+  if (LOWL) {
+    U.lowbitmap = L.lowbitmap + L.word_off[o] + (long long)(s_first - 1) * oc.h * U.nw;
+    U.lowrowcount = L.lowrowcount + L.row_off[o] + (s_first - 1) * oc.h;
+  }
   U.low = 0;
 
   XWin<NP> Wn;
@@ -150,15 +170,15 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   for (int y = y0; y <= y1; y += 3) {
     x_derive<NP, 1>(Wn, Wn.raw[1]);
     x_load(U, Wn.raw[1], min(y + 4, y1 + 1));
-    x_centre<NP, 2, 0, 1>(Wn, U, L, y);
+    x_centre<NP, 2, 0, 1, LOWL>(Wn, U, L, y);
     if (y + 1 > y1) break;
     x_derive<NP, 2>(Wn, Wn.raw[2]);
     x_load(U, Wn.raw[2], min(y + 5, y1 + 1));
-    x_centre<NP, 0, 1, 2>(Wn, U, L, y + 1);
+    x_centre<NP, 0, 1, 2, LOWL>(Wn, U, L, y + 1);
     if (y + 2 > y1) break;
     x_derive<NP, 0>(Wn, Wn.raw[0]);
     x_load(U, Wn.raw[0], min(y + 6, y1 + 1));
-    x_centre<NP, 1, 2, 0>(Wn, U, L, y + 2);
+    x_centre<NP, 1, 2, 0, LOWL>(Wn, U, L, y + 2);
   }
   if (U.lane == 0 && U.low) atomicAdd(&L.counters[1], U.low);
 }
@@ -167,6 +187,8 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
 // group): all DoG planes of the group stream through once, each plane's row
 // is reduced once (3-wide max/min with DPP shifts) and shared by the scales
 // above and below it; the decisions are SALU lane-mask logic.
+// LOWL: also the bitmap of the certain low-contrast extrema (their list).
+template <bool LOWL>
 __global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
   const int u = L.u_begin + (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (u >= L.u_end) return;
@@ -182,11 +204,11 @@ __global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaL
   const int s_first = 1 + g * per + min(g, rem);
   const int cnt = per + (g < rem ? 1 : 0);
   switch (cnt) {
-    case 1: x_scan<3>(P, L, o, s_first, xw, y0, y1); break;
-    case 2: x_scan<4>(P, L, o, s_first, xw, y0, y1); break;
-    case 3: x_scan<5>(P, L, o, s_first, xw, y0, y1); break;
-    case 4: x_scan<6>(P, L, o, s_first, xw, y0, y1); break;
-    default: x_scan<7>(P, L, o, s_first, xw, y0, y1); break;
+    case 1: x_scan<3, LOWL>(P, L, o, s_first, xw, y0, y1); break;
+    case 2: x_scan<4, LOWL>(P, L, o, s_first, xw, y0, y1); break;
+    case 3: x_scan<5, LOWL>(P, L, o, s_first, xw, y0, y1); break;
+    case 4: x_scan<6, LOWL>(P, L, o, s_first, xw, y0, y1); break;
+    default: x_scan<7, LOWL>(P, L, o, s_first, xw, y0, y1); break;
   }
 }
 
@@ -232,7 +254,7 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
       if (pos < E.cap) {
         E.keys[pos] = kbase + (unsigned)x;
         E.value[pos] = (double)Dc[x];
-        E.keep[pos] = 1u;
+        if (E.keep) E.keep[pos] = 1u;
       }
       ++pos;
     }
@@ -274,7 +296,16 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
       const bool cand = ext && fabs(v) >= P.pix_thr;
       X.keep[idx] = cand ? 1u : 0u;
       X.value[idx] = v;
-      if (ext && !cand) atomicAdd(&X.counters[1], 1u);
+      if (ext && !cand) {
+        atomicAdd(&X.counters[1], 1u);
+        if (X.late_keys) {  // decided low contrast here: joins the low-contrast list
+          const unsigned slot = atomicAdd(&X.counters[6], 1u);
+          if (slot < X.amb_cap) {
+            X.late_keys[slot] = key;
+            X.late_vals[slot] = v;
+          }
+        }
+      }
       if (!cand) atomicAdd(&X.counters[2], 1u);  // dropped entries
     }
     __syncthreads();  // smem is reused by the next key
@@ -306,11 +337,13 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
     const long v = e ? std::strtol(e, nullptr, 10) : 0;
     return (v > 0 && v <= 160 * 1024) ? (int)v : 0;
   }();
+  const void* fn = L.lowbitmap ? (const void*)k_extrema<true> : (const void*)k_extrema<false>;
   if (xlds > 65536) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_extrema, hipFuncAttributeMaxDynamicSharedMemorySize, xlds);
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, xlds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_extrema, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), xlds, st, P, L);
+  if (L.lowbitmap) hipLaunchKernelGGL(k_extrema<true>, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), xlds, st, P, L);
+  else hipLaunchKernelGGL(k_extrema<false>, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), xlds, st, P, L);
   return hipGetLastError();
 }
 

@@ -75,6 +75,8 @@ struct ExtremaLaunch {
   unsigned* amb_keys;            // keys needing an exact fp64 decision (unordered)
   unsigned* counters;            // [0] ambiguous, [1] low-contrast, [2] dropped by exact pass
   unsigned amb_cap;
+  unsigned long long* lowbitmap; // certain low-contrast extrema, same layout as bitmap (nullptr = not listed)
+  unsigned* lowrowcount;
 };
 
 // One launch over every octave: global row g (one wave each) = row_off[o] +
@@ -91,7 +93,7 @@ struct EmitLaunch {
   const unsigned* rowoff;        // exclusive scan of rowcount
   unsigned* keys;                // ordered candidate keys
   double* value;
-  unsigned* keep;
+  unsigned* keep;                // nullptr: not written
   unsigned cap;                  // slots in keys/value/keep (overflow is detected by the host)
 };
 
@@ -103,7 +105,9 @@ struct ExactLaunch {
   unsigned cap;
   unsigned* keep;
   double* value;
-  unsigned* counters;
+  unsigned* counters;            // [6]: late low-contrast extrema (ambiguous ones decided low)
+  unsigned* late_keys;           // their keys / exact values (nullptr = not listed), amb_cap slots
+  double* late_vals;
 };
 
 struct RefineLaunch {

@@ -76,13 +76,17 @@ __device__ __forceinline__ void x_derive(XWin<NP>& Wn, const float (&src)[NP]) {
 // values tie; ties and |v| within fp32 rounding of 0.8 thr (c_lo <= |v| <
 // c_hi) are ambiguous: kept in the candidate bitmap and their keys (key of
 // this lane) appended for the exact fp64 pass.  Certain low-contrast extrema
-// are counted into `low`.  Returns the candidate lanes (ambiguous included).
+// are counted into `low` and returned in `lowmask` (the reference's
+// lowContrastKeypoints, sift.js:293-306).  Returns the candidate lanes
+// (ambiguous included).
 // Most rows of a word hold no extremum at a given scale: one ballot decides,
 // the rest is skipped (lane-mask logic in SALU).
 __device__ __forceinline__ unsigned long long x_row_decide(float v, float nmax, float nmin,
                                                            unsigned long long colmask, float c_lo, float c_hi,
                                                            bool exact_planes, unsigned key, unsigned* amb_count,
-                                                           unsigned* amb_keys, unsigned amb_cap, unsigned& low) {
+                                                           unsigned* amb_keys, unsigned amb_cap, unsigned& low,
+                                                           unsigned long long& lowmask) {
+  lowmask = 0ull;
   const unsigned long long ext_any = __ballot(v >= nmax || v <= nmin) & colmask;
   if (!ext_any) return 0ull;
   const float av = __builtin_fabsf(v);
@@ -96,6 +100,7 @@ __device__ __forceinline__ unsigned long long x_row_decide(float v, float nmax, 
   const unsigned long long bit = ext & ~count_low;
   const unsigned long long amb = bit & (tie | ~hi);
   low += (unsigned)__popcll(count_low);
+  lowmask = count_low;
   if (amb) {  // rare: ties / contrast within fp32 rounding of the threshold
     const bool mine = (amb >> (threadIdx.x & 63)) & 1ull;
     const unsigned slot = wave_append(mine, amb_count);

@@ -284,22 +284,28 @@ export function findCandidateKeypoints(args, octave_base_images, scales_per_octa
   }
   const { differenceOfGaussians, scalesPerOctave, device = 0 } = a;  // octaveBaseImages: unused (background.js:361)
   const st = ensureDog(differenceOfGaussians, scalesPerOctave, device);
-  const r = native.findExtrema(st.ctx);
+  const r = native.findExtrema(st.ctx, true);
   const O = differenceOfGaussians.length;
   const S = differenceOfGaussians[0].length - 2;
-  const out = [];
-  for (let o = 0; o < O; o++) {
-    const oct = [];
-    for (let s = 1; s <= S; s++) oct.push({ scaleLevel: s, localExtremas: [] });
-    out.push(oct);
-  }
-  const n = r.values.length;
-  for (let i = 0; i < n; i++) {
-    const o = r.ints[4 * i], s = r.ints[4 * i + 1];
-    out[o][s - 1].localExtremas.push({ x: r.ints[4 * i + 2], y: r.ints[4 * i + 3], value: r.values[i] });
-  }
+  const group = (ints, values) => {  // [octave][scale-1] = {scaleLevel, localExtremas: [{x, y, value}]}
+    const out = [];
+    for (let o = 0; o < O; o++) {
+      const oct = [];
+      for (let s = 1; s <= S; s++) oct.push({ scaleLevel: s, localExtremas: [] });
+      out.push(oct);
+    }
+    for (let i = 0; i < values.length; i++) {
+      const o = ints[4 * i], s = ints[4 * i + 1];
+      out[o][s - 1].localExtremas.push({ x: ints[4 * i + 2], y: ints[4 * i + 3], value: values[i] });
+    }
+    return out;
+  };
+  const out = group(r.ints, r.values);
   Object.defineProperty(out, 'lowContrastCount', { value: r.lowContrast, enumerable: false });
-  return attach(out, st, st.gen, { n });
+  // SIFT_findExtremas' lowContrastKeypoints (sift.js:293-306), same shape; the
+  // reference does not return them, it posts one marker each (background.js:408-413)
+  Object.defineProperty(out, 'lowContrastKeypoints', { value: group(r.lowInts, r.lowValues), enumerable: false });
+  return attach(out, st, st.gen, { n: r.values.length });
 }
 
 // ---------------------------------------------------------------------------
@@ -441,18 +447,36 @@ export function planeImageData(pyramid, octave, scale, { mode = 'plain', coeffic
   return { width: cols, height: rows, data: native.planeImage(h.st.ctx, h.kind, octave, scale, m, coefficient) };
 }
 
+// Chunk previews (background.js:181-203, :294-321): crops of a plane preview
+// over ImageUtils_generateChunkBoundaries' tiles (image-utils.js:295-332:
+// x-major, the last tile of a row / column shortened to the image).
+function postChunks(post, type, img, chunk) {
+  const { width: W, height: H, data } = img;
+  for (let x = 0; x < W; x += chunk) {
+    const cw = x + chunk >= W ? W - x : chunk;
+    for (let y = 0; y < H; y += chunk) {
+      const ch = y + chunk >= H ? H - y : chunk;
+      const out = new Uint8ClampedArray(cw * ch * 4);
+      for (let r = 0; r < ch; r++) out.set(data.subarray(((y + r) * W + x) * 4, ((y + r) * W + x + cw) * 4), r * cw * 4);
+      post({ type, imageData: { width: cw, height: ch, data: out }, dx: x, dy: y });
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // background.js-compatible dispatcher (background.js:14-50): returns an
 // onmessage(e) that answers each request with the reference's RECEIVED_*
 // message.  Pyramids go out as Matrix2D by default, as the reference posts
-// them (main.js indexes image[y][x]).  With {previews: true} the per-plane
-// preview messages are posted too, in the reference's order, with device-
-// made ImageData (RECEIVED_GAUSSIAN_BLURRED_IMAGE, _DIFFERENCE_OF_GAUSSIAN_
-// IMAGE, _CANDIDATE_KEYPOINT_BASE_IMAGE, candidate markers, _CANDIDATE_
-// KEYPOINT_IMAGE).  Not emitted: per-chunk previews (crops of the plane
-// previews) and low-contrast markers (only their count is kept on device).
+// them (main.js indexes image[y][x]).  With {previews: true} every progress
+// message of the reference is posted too, in its order, with device-made
+// ImageData: per-chunk and per-plane Gaussian previews
+// (RECEIVED_GAUSSIAN_BLURRED_CHUNK / _IMAGE), per-chunk sigmoid(5) and
+// per-plane sampled DoG previews (RECEIVED_DIFFERENCE_OF_GAUSSIAN_CHUNK /
+// _IMAGE), and per (octave, scale) the sampled base image, the low-contrast
+// markers, the candidate markers and RECEIVED_CANDIDATE_KEYPOINT_IMAGE.
+// {chunks: false} leaves out the per-chunk messages.
 // ---------------------------------------------------------------------------
-export function createWorkerHandler(post, { matrix2d = true, device = 0, previews = false } = {}) {
+export function createWorkerHandler(post, { matrix2d = true, device = 0, previews = false, chunks = true } = {}) {
   return (e) => {
     const m = e && e.data !== undefined ? e.data : e;
     switch (m.type) {
@@ -460,21 +484,28 @@ export function createWorkerHandler(post, { matrix2d = true, device = 0, preview
         const scaleSpace = computeGaussianScaleSpace({ input_image: m.inputImage, number_of_octaves: m.numberOfOctaves,
           scales_per_octave: m.scalesPerOctave, min_blur_level: m.minBlurLevel, assumed_blur: m.assumedBlur,
           chunk_size: m.chunkSize, matrix2d, device });
-        if (previews) {  // background.js:137-141 / :216-221
-          scaleSpace.forEach((oct, o) => oct.forEach((_, s) => post({
-            type: WorkerMessageTypes.RECEIVED_GAUSSIAN_BLURRED_IMAGE, imageData: planeImageData(scaleSpace, o, s), octave: o,
-          })));
+        if (previews) {  // background.js:136-143 (octave seeds), :194-202 (chunks), :215-222 (planes)
+          const chunk = m.chunkSize || 32;
+          scaleSpace.forEach((oct, o) => oct.forEach((_, s) => {
+            const img = planeImageData(scaleSpace, o, s);
+            if (chunks && !(o > 0 && s === 0)) postChunks(post, WorkerMessageTypes.RECEIVED_GAUSSIAN_BLURRED_CHUNK, img, chunk);
+            post({ type: WorkerMessageTypes.RECEIVED_GAUSSIAN_BLURRED_IMAGE, imageData: img, octave: o });
+          }));
         }
         post({ type: WorkerMessageTypes.RECEIVED_GAUSSIAN_SCALE_SPACE, scaleSpace });
         break;
       }
       case WorkerMessageTypes.COMPUTE_DIFFERENCE_OF_GAUSSIANS: {
         const dog = computeDifferenceOfGaussians(m.scaleSpace, 32, { device, matrix2d });
-        if (previews) {  // background.js:333-338
-          dog.forEach((oct, o) => oct.forEach((_, s) => post({
-            type: WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIAN_IMAGE,
-            imageData: planeImageData(dog, o, s, { mode: 'sampled' }), octave: o,
-          })));
+        if (previews) {  // background.js:303-320 (sigmoid chunks, chunk size 32), :333-339 (sampled planes)
+          dog.forEach((oct, o) => oct.forEach((_, s) => {
+            if (chunks) {
+              postChunks(post, WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIAN_CHUNK,
+                planeImageData(dog, o, s, { mode: 'sigmoid', coefficient: 5 }), 32);
+            }
+            post({ type: WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIAN_IMAGE,
+              imageData: planeImageData(dog, o, s, { mode: 'sampled' }), octave: o });
+          }));
         }
         post({ type: WorkerMessageTypes.RECEIVED_DIFFERENCE_OF_GAUSSIANS, differenceOfGaussians: dog });
         break;
@@ -483,9 +514,13 @@ export function createWorkerHandler(post, { matrix2d = true, device = 0, preview
         const candidateKeypoints = findCandidateKeypoints({ ...m, device });
         if (previews) {  // background.js:380-429
           const dogs = m.differenceOfGaussians;
-          candidateKeypoints.forEach((oct, o) => oct.forEach((sc) => {
+          const low = candidateKeypoints.lowContrastKeypoints;
+          candidateKeypoints.forEach((oct, o) => oct.forEach((sc, j) => {
             post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINT_BASE_IMAGE,
               imageData: planeImageData(dogs, o, sc.scaleLevel, { mode: 'sampled' }) });
+            for (const x of low[o][j].localExtremas) {
+              post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINT_MARKER, x: x.x, y: x.y, isLowContrast: true });
+            }
             for (const x of sc.localExtremas) {
               post({ type: WorkerMessageTypes.RECEIVED_CANDIDATE_KEYPOINT_MARKER, x: x.x, y: x.y, isLowContrast: false });
             }

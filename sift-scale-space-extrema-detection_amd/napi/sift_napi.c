@@ -44,6 +44,7 @@ static napi_value throw_sift(napi_env env, struct sift_ctx *ctx, int rc, const c
 typedef struct {
   struct sift_ctx *ctx;
   int busy;
+  int flags;  /* sift_params.flags of the last build / load through this handle */
 } ctx_box;
 
 static void ctx_finalize(napi_env env, void *data, void *hint) {
@@ -202,6 +203,7 @@ static napi_value js_build(napi_env env, napi_callback_info info) {
   if (argc > 5) sig = (const double *)typed_data(env, argv[5], napi_float64_array, NULL);
   int rc = sift_build_scale_space(ctx, img, w, h, (size_t)w, &p, sig);
   if (rc) return throw_sift(env, ctx, rc, "sift_build_scale_space");
+  get_box(env, argv[0])->flags = p.flags;
   return NULL;
 }
 
@@ -285,20 +287,49 @@ static napi_value load_common(napi_env env, napi_callback_info info, int which) 
   }
   int rc = which ? sift_load_scale_space(ctx, flat, w, h, &p) : sift_load_dog(ctx, flat, w, h, &p);
   if (rc) return throw_sift(env, ctx, rc, which ? "sift_load_scale_space" : "sift_load_dog");
+  get_box(env, argv[0])->flags = p.flags;
   return NULL;
 }
 static napi_value js_load_dog(napi_env env, napi_callback_info info) { return load_common(env, info, 0); }
 static napi_value js_load_ss(napi_env env, napi_callback_info info) { return load_common(env, info, 1); }
 
-/* findExtrema(ctx) -> {ints: Int32Array(4n) [o,s,x,y], values: Float64Array(n), lowContrast} */
+/* extremum records -> {ints: Int32Array(4n) [o,s,x,y], values: Float64Array(n)} set on `out` as ints/values
+ * (or lowInts/lowValues) */
+static void extrema_to_js(napi_env env, const sift_extremum *e, size_t n, napi_value out, const char *ki,
+                          const char *kv) {
+  int32_t *ints;
+  double *vals;
+  napi_value ia = make_typed(env, napi_int32_array, 4 * n, 4, (void **)&ints);
+  napi_value va = make_typed(env, napi_float64_array, n, 8, (void **)&vals);
+  for (size_t i = 0; i < n; ++i) {
+    ints[4 * i] = e[i].octave;
+    ints[4 * i + 1] = e[i].scale;
+    ints[4 * i + 2] = e[i].x;
+    ints[4 * i + 3] = e[i].y;
+    vals[i] = e[i].value;
+  }
+  napi_set_named_property(env, out, ki, ia);
+  napi_set_named_property(env, out, kv, va);
+}
+
+/* findExtrema(ctx, wantLow) -> {ints: Int32Array(4n) [o,s,x,y], values: Float64Array(n), lowContrast,
+ *                               lowInts?, lowValues? (the low-contrast list, wantLow)} */
 static napi_value js_find_extrema(napi_env env, napi_callback_info info) {
-  size_t argc = 1;
-  napi_value argv[1];
+  size_t argc = 2;
+  napi_value argv[2];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  struct sift_ctx *ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
+  ctx_box *box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  struct sift_ctx *ctx = box->ctx;
+  bool want_low = false;
+  if (argc > 1) napi_get_value_bool(env, argv[1], &want_low);
   size_t n = 0, low = 0;
+  if (want_low) {
+    /* the pyramid's flags + SIFT_F_LOW_CONTRAST_LIST for this extrema stage */
+    sift_set_flags(ctx, box->flags | SIFT_F_LOW_CONTRAST_LIST);
+  }
   int rc = sift_find_extrema(ctx, NULL, 0, &n, &low);
+  if (want_low) sift_set_flags(ctx, box->flags);
   if (rc) return throw_sift(env, ctx, rc, "sift_find_extrema");
   sift_extremum *tmp = (sift_extremum *)malloc(sizeof(sift_extremum) * (n ? n : 1));
   rc = sift_copy_candidates(ctx, tmp, n, &n);
@@ -306,24 +337,25 @@ static napi_value js_find_extrema(napi_env env, napi_callback_info info) {
     free(tmp);
     return throw_sift(env, ctx, rc, "sift_copy_candidates");
   }
-  int32_t *ints;
-  double *vals;
-  napi_value ia = make_typed(env, napi_int32_array, 4 * n, 4, (void **)&ints);
-  napi_value va = make_typed(env, napi_float64_array, n, 8, (void **)&vals);
-  for (size_t i = 0; i < n; ++i) {
-    ints[4 * i] = tmp[i].octave;
-    ints[4 * i + 1] = tmp[i].scale;
-    ints[4 * i + 2] = tmp[i].x;
-    ints[4 * i + 3] = tmp[i].y;
-    vals[i] = tmp[i].value;
-  }
-  free(tmp);
   napi_value out, lv;
   napi_create_object(env, &out);
-  napi_set_named_property(env, out, "ints", ia);
-  napi_set_named_property(env, out, "values", va);
+  extrema_to_js(env, tmp, n, out, "ints", "values");
+  free(tmp);
   napi_create_double(env, (double)low, &lv);
   napi_set_named_property(env, out, "lowContrast", lv);
+  if (want_low) {
+    size_t nl = 0;
+    rc = sift_copy_low_contrast(ctx, NULL, 0, &nl);
+    if (rc) return throw_sift(env, ctx, rc, "sift_copy_low_contrast");
+    sift_extremum *lt = (sift_extremum *)malloc(sizeof(sift_extremum) * (nl ? nl : 1));
+    rc = sift_copy_low_contrast(ctx, lt, nl, &nl);
+    if (rc) {
+      free(lt);
+      return throw_sift(env, ctx, rc, "sift_copy_low_contrast");
+    }
+    extrema_to_js(env, lt, nl, out, "lowInts", "lowValues");
+    free(lt);
+  }
   return out;
 }
 
@@ -607,6 +639,7 @@ static napi_value js_build_rgba(napi_env env, napi_callback_info info) {
   if (argc > 5) sig = (const double *)typed_data(env, argv[5], napi_float64_array, NULL);
   int rc = sift_build_scale_space_rgba(ctx, rgba, w, h, (size_t)w * 4, &p, sig);
   if (rc) return throw_sift(env, ctx, rc, "sift_build_scale_space_rgba");
+  get_box(env, argv[0])->flags = p.flags;
   return NULL;
 }
 

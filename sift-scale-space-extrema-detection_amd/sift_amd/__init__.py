@@ -30,6 +30,7 @@ F_SKIP_GAUSS_PLANES = 1
 F_EXPORT_NEXT_SEED = 4
 F_KEYPOINT_ORIGINS = 8
 F_FUSED_EXTREMA = 16
+F_LOW_CONTRAST_LIST = 32
 
 AFTER_OCTAVE0 = 0
 AFTER_GAUSSIAN = 1
@@ -55,7 +56,7 @@ ABI_SYMBOLS = (
     "sift_plane_image", "sift_plane_image_device", "sift_detect_begin_async", "sift_detect_end_async",
     "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device", "sift_last_octave_timings",
     "sift_detect_from_seed_range_device", "sift_merge_keypoint_blocks_device", "sift_set_owned_rows",
-    "sift_last_block_counts",
+    "sift_last_block_counts", "sift_copy_low_contrast", "sift_set_flags",
 )
 
 
@@ -141,6 +142,8 @@ def lib():
         "sift_set_candidates": (ctypes.c_int, [vp, vp, sz]),
         "sift_refine_params": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double]),
         "sift_copy_candidates": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_copy_low_contrast": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_set_flags": (ctypes.c_int, [vp, ctypes.c_int]),
         "sift_copy_keypoints": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_copy_keypoints_device": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_detect": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
@@ -325,6 +328,19 @@ class Context:
         out = np.zeros(max(n.value, 1), dtype=EXTREMUM_DTYPE)
         self._check(self._L.sift_copy_candidates(self._h, out.ctypes.data_as(ctypes.c_void_p), out.shape[0],
                                                  ctypes.byref(n)), "sift_copy_candidates")
+        return out[:n.value]
+
+    def set_flags(self, flags):
+        """Replace the current pyramid's sift_params.flags for the following stages."""
+        self._check(self._L.sift_set_flags(self._h, int(flags)), "sift_set_flags")
+
+    def low_contrast(self):
+        """Low-contrast extrema of the last extrema stage (params with F_LOW_CONTRAST_LIST), reference order."""
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_copy_low_contrast(self._h, None, 0, ctypes.byref(n)), "sift_copy_low_contrast")
+        out = np.zeros(max(n.value, 1), dtype=EXTREMUM_DTYPE)
+        self._check(self._L.sift_copy_low_contrast(self._h, out.ctypes.data_as(ctypes.c_void_p), out.shape[0],
+                                                   ctypes.byref(n)), "sift_copy_low_contrast")
         return out[:n.value]
 
     def keypoints(self):

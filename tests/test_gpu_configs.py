@@ -31,10 +31,15 @@ pytestmark = pytest.mark.gpu
 
 
 def _vs_oracle(ctx, img, p, mode, low_rtol=0.0):
+    """low_rtol == 0: the low-contrast list (F_LOW_CONTRAST_LIST) must equal
+    the oracle's too (positions exact, values within fp32 rounding)."""
     t0 = time.perf_counter()
+    p = sift_amd.make_params(p.num_octaves, p.scales_per_octave, p.min_blur, p.assumed_blur,
+                             p.min_interpixel_distance, p.flags | sift_amd.F_LOW_CONTRAST_LIST)
     kp = ctx.detect(img, p).copy()
     cand = ctx.candidates()
     counts = ctx.counts()
+    low = ctx.low_contrast()
     t1 = time.perf_counter()
     r = orc.OracleRun(img, oracle_params(p), mode, threads=host_threads(), keep_gauss=False)
     t2 = time.perf_counter()
@@ -52,6 +57,9 @@ def _vs_oracle(ctx, img, p, mode, low_rtol=0.0):
     check_candidates(cand, r.candidates())
     check_keypoints(kp, r.refined)
     assert abs(counts["low_contrast"] - r.n_low) <= low_rtol * r.n_low, (counts["low_contrast"], r.n_low)
+    assert low.shape[0] == counts["low_contrast"]
+    if low_rtol == 0.0:
+        check_candidates(low, r.low_contrast())
     assert counts["singular"] == r.n_singular == 0
     return kp, r
 

@@ -33,12 +33,18 @@ def params_of(g, flags=0):
 @pytest.mark.parametrize("name", case_names())
 def test_detect_matches_reference(gpu_ctx, name):
     g = Golden(name)
-    kp = gpu_ctx.detect(g.img, params_of(g))
+    kp = gpu_ctx.detect(g.img, params_of(g, sift_amd.F_LOW_CONTRAST_LIST))
     check_candidates(gpu_ctx.candidates(), g.candidates)
     check_keypoints(kp, g.refined)
     cnt = gpu_ctx.counts()
     assert cnt["low_contrast"] == int(g.z["low_contrast_counts"].sum())
     assert cnt["singular"] == 0
+    # per (octave, scale) low-contrast counts of the reference (background.js:408-413 markers)
+    low = gpu_ctx.low_contrast()
+    per = np.zeros_like(np.asarray(g.z["low_contrast_counts"]).ravel())
+    S = g.params["scales_per_octave"]
+    np.add.at(per, low["octave"] * S + low["scale"] - 1, 1)
+    np.testing.assert_array_equal(per, np.asarray(g.z["low_contrast_counts"]).ravel())
 
 
 @pytest.mark.parametrize("name", case_names())
@@ -73,12 +79,42 @@ def test_stage_api_matches_reference(gpu_ctx, name):
 @pytest.mark.parametrize("W,H,O,S,seed", [(1920, 1080, 4, 5, 11), (640, 480, 5, 3, 12), (333, 517, 4, 4, 13)])
 def test_detect_matches_oracle_large(gpu_ctx, W, H, O, S, seed):
     img = blob_image(W, H, seed=seed)
-    p = sift_amd.make_params(O, S)
+    p = sift_amd.make_params(O, S, flags=sift_amd.F_LOW_CONTRAST_LIST)
     kp = gpu_ctx.detect(img, p)
     r = orc.OracleRun(img, _oracle_params(p), orc.CONV_SEPARABLE)
     check_candidates(gpu_ctx.candidates(), r.candidates())
     check_keypoints(kp, r.refined)
     assert gpu_ctx.counts()["low_contrast"] == r.n_low
+    # the reference's lowContrastKeypoints (sift.js:293-306), in its order
+    check_candidates(gpu_ctx.low_contrast(), r.low_contrast())
+
+
+def test_low_contrast_list_stage_api_and_flags(gpu_ctx):
+    """The low-contrast list through the stage API (sift_set_flags before
+    sift_find_extrema on a built pyramid) and on a caller-supplied DoG
+    (exact planes), against the oracle; without the flag it is refused."""
+    img = blob_image(300, 220, seed=27)
+    p = sift_amd.make_params(4, 4)
+    r = orc.OracleRun(img, _oracle_params(p), orc.CONV_SEPARABLE)
+    gpu_ctx.build_scale_space(img, p)
+    gpu_ctx.find_extrema()
+    with pytest.raises(sift_amd.SiftError):
+        gpu_ctx.low_contrast()
+    gpu_ctx.set_flags(sift_amd.F_LOW_CONTRAST_LIST)
+    cand, low = gpu_ctx.find_extrema()
+    check_candidates(cand, r.candidates())
+    lc = gpu_ctx.low_contrast()
+    assert lc.shape[0] == low == r.n_low
+    check_candidates(lc, r.low_contrast())
+    # caller-supplied fp32 DoG planes: every decision is on those planes
+    dog32 = r.dog_flat.astype(np.float32)
+    gpu_ctx.load_dog(dog32, 300, 220, sift_amd.make_params(4, 4, flags=sift_amd.F_LOW_CONTRAST_LIST))
+    cand2, low2 = gpu_ctx.find_extrema()
+    (crec, cval), (lrec, lval) = orc.extrema_lists(_oracle_params(p), 300, 220, dog32.astype(np.float64))
+    check_candidates(cand2, orc.as_records(crec, cval))
+    lc2 = gpu_ctx.low_contrast()
+    assert lc2.shape[0] == low2 == lrec.shape[0]
+    check_candidates(lc2, orc.as_records(lrec, lval))
 
 
 def test_foreign_dog_is_exact(gpu_ctx):

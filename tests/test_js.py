@@ -130,3 +130,53 @@ def test_js_image_products_match_reference():
     assert (fp["octave"], fp["w"], fp["h"]) == (0, 2 * W, 2 * H)
     ref = ip.gray_image_data(np.array(out["gaussPlane00"], np.float64))
     np.testing.assert_array_equal(np.array(fp["px"], np.uint8).reshape(4, 4), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["messages_blob64x48_o3_s3", "messages_blob77x51_o3_s4_c20"])
+def test_js_worker_message_stream_matches_reference(name):
+    """The worker shim with previews posts the reference worker's message
+    stream: every message type in order (chunk and plane previews of the
+    Gaussian and DoG stages, base images, low-contrast and candidate markers,
+    results), every scalar field (octave, dx / dy chunk origins, marker x / y
+    and isLowContrast), the list sizes, and every ImageData's dimensions and
+    bytes -- captured from the unmodified reference by
+    tests/golden/make_messages_golden.py.  Preview bytes are made from the
+    fp32 planes, the reference's from fp64: a byte may differ by one level
+    where v*255 lies within fp32 rounding of a rounding boundary."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sift-scale-space-extrema-detection_amd"))
+    from sift_amd.synth import blob_image
+    z = np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"))
+    ref = json.loads(str(z["meta"]))
+    ref_bytes = z["bytes"]
+    p = json.loads(str(z["params"]))
+    spec = json.loads(str(z["image_spec"]))
+    img = blob_image(spec["width"], spec["height"], seed=spec["seed"])
+    with tempfile.TemporaryDirectory() as td:
+        img.tofile(os.path.join(td, "in.f32"))
+        with open(os.path.join(td, "p.json"), "w") as f:
+            json.dump(p, f)
+        r = subprocess.run([NODE, os.path.join(ROOT, "tests", "js", "run_worker_messages.mjs"),
+                            os.path.join(td, "in.f32"), os.path.join(td, "p.json"), os.path.join(td, "m.json"),
+                            os.path.join(td, "m.u8")], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        got = json.load(open(os.path.join(td, "m.json")))
+        got_bytes = np.fromfile(os.path.join(td, "m.u8"), dtype=np.uint8)
+    assert [m["type"] for m in got] == [m["type"] for m in ref]
+    n_low = sum(1 for m in ref if m.get("isLowContrast") is True)
+    assert n_low > 0
+    diff_px = 0
+    total = 0
+    for a, b in zip(got, ref):
+        for k in ("octave", "dx", "dy", "x", "y", "isLowContrast", "w", "h", "n"):
+            assert a.get(k) == b.get(k), (b["type"], k, a.get(k), b.get(k))
+        if "off" in b:
+            n = 4 * b["w"] * b["h"]
+            ga = got_bytes[a["off"]:a["off"] + n].astype(np.int16)
+            ra = ref_bytes[b["off"]:b["off"] + n].astype(np.int16)
+            d = np.abs(ga - ra)
+            assert d.max() <= 1, (b["type"], int(d.max()))
+            diff_px += int((d > 0).sum())
+            total += n
+    assert diff_px <= 1e-3 * total, (diff_px, total)
