@@ -46,7 +46,7 @@ out.ssSampleGray = Array.from(ssg[1][2].image.data.subarray(0, 32));
 
 // worker protocol with previews (background.js message order)
 const posted = [];
-const onmessage = sift.createWorkerHandler(m => posted.push(m), { matrix2d: true, previews: true });
+const onmessage = sift.createWorkerHandler(m => posted.push(m), { matrix2d: true, previews: true, chunks: false });
 onmessage({ data: { type: sift.WorkerMessageTypes.COMPUTE_GAUSSIAN_SCALE_SPACE, inputImage: imageData,
   numberOfOctaves: 3, scalesPerOctave: 3, minBlurLevel: 0.8, assumedBlur: 0.5, chunkSize: 32 } });
 const wss = posted[posted.length - 1].scaleSpace;
@@ -59,6 +59,7 @@ let nc = 0;
 cc.forEach(o => o.forEach(s => { nc += s.localExtremas.length; }));
 out.worker = {
   types: posted.map(m => m.type), candidates: nc,
+  lowMarkers: posted.filter(m => m.type === 'received-candidate-keypoint-marker' && m.isLowContrast).length,
   firstGaussPreview: (() => { const m = posted[0]; return { octave: m.octave, w: m.imageData.width, h: m.imageData.height,
     px: Array.from(m.imageData.data.subarray(0, 16)) }; })(),
 };
