@@ -121,6 +121,35 @@ def cpu_baseline(img_full, O, S, sample_w, sample_h, threads=1):
                                                 else "", dt, nk)}
 
 
+def cpu_baseline_js(img_full, O, S, sample_w, sample_h):
+    """a clean-room single-threaded JavaScript
+    restatement of the reference's 2D-kernel algorithm (tools/js_restatement/
+    sift_restated.mjs, pinned to the reference's golden lists by
+    tests/test_js_restatement.py), timed under the host's Node on a crop."""
+    import shutil
+    import subprocess
+    import tempfile
+    import numpy as np
+    node = shutil.which("node")
+    if node is None:
+        return None
+    crop = np.ascontiguousarray(img_full[:sample_h, :sample_w], dtype="<f4")
+    with tempfile.TemporaryDirectory() as td:
+        crop.tofile(os.path.join(td, "img.f32"))
+        r = subprocess.run([node, os.path.join(ROOT, "tools", "js_restatement", "sift_restated.mjs"),
+                            os.path.join(td, "img.f32"), str(sample_w), str(sample_h), str(O), str(S)],
+                           capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"value": None, "error": r.stderr[-300:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": round(sample_w * sample_h / d["seconds"] / 1e6, 6), "unit": "Mpix/s", "cores": 1,
+            "kind": "restatement",
+            "sample": "%dx%d crop of the same synthetic image, %d oct x %d scales, G+DoG+extrema+refine, "
+                      "reference 2D-kernel algorithm restated in JavaScript (tools/js_restatement/sift_restated.mjs, "
+                      "flat Float64Array planes), Node %s, one thread, %.1f s, %d keypoints"
+                      % (sample_w, sample_h, O, S, d["node"], d["seconds"], d["keypoints"])}
+
+
 def host_cores():
     """CPU threads this process may use (the GPU box's share is 16)."""
     try:
@@ -164,6 +193,8 @@ def main():
                          "unless --width/--height/--octaves are given")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
+    ap.add_argument("--cpu-sample-js", default="960x540",
+                    help="crop WxH timed on the single-threaded JS restatement (about 20 s at 960x540)")
     args = ap.parse_args()
     big = args.shard_image
     args.width = args.width or (7680 if big else 3840)
@@ -400,6 +431,7 @@ def main():
             },
             "cpu_baseline": None,
             "cpu_baseline_all_cores": None,
+            "cpu_baseline_js": None,
         }
         if world == 1 and not args.no_cpu_baseline:
             sw, sh = (int(v) for v in args.cpu_sample.split("x"))
@@ -407,6 +439,8 @@ def main():
             nt = host_cores()
             if nt > 1:  # the port on 1 core and on all the cores this process may use
                 out["cpu_baseline_all_cores"] = cpu_baseline(img, O, S, min(sw, W), min(sh, H), threads=nt)
+            jw, jh = (int(v) for v in args.cpu_sample_js.split("x"))
+            out["cpu_baseline_js"] = cpu_baseline_js(img, O, S, min(jw, W), min(jh, H))
         print(json.dumps(out), flush=True)
     for c in reversed(ctxs):
         c.close()
