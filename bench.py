@@ -193,8 +193,8 @@ def main():
                          "unless --width/--height/--octaves are given")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
-    ap.add_argument("--cpu-sample-js", default="960x540",
-                    help="crop WxH timed on the single-threaded JS restatement (about 20 s at 960x540)")
+    ap.add_argument("--cpu-sample-js", default="1920x1080",
+                    help="crop WxH timed on the single-threaded JS restatement (the C port's crop; about 15 s on the GPU box)")
     args = ap.parse_args()
     big = args.shard_image
     args.width = args.width or (7680 if big else 3840)

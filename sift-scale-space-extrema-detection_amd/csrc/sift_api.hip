@@ -52,7 +52,7 @@ enum DogSource { kNone = 0, kNative = 1, kForeign = 2 };
 // Device counter slots: 0..31 extrema / refinement counts (see below), then
 // the kept keypoints per (octave, scale) block from kBlk on.
 constexpr int kBlk = 64;
-constexpr int kCntAll = kBlk + kMaxOctaves * kMaxScales;
+constexpr int kCntAll = kBlk + kBlkWords;  // per-block counts, block starts, order flag (sift_kernels.h)
 
 }  // namespace
 
@@ -980,7 +980,8 @@ static int refine_enqueue(sift_ctx* ctx) {
                                             ctx->stream));
     HIPCHK(launch_scatter_keypoints(ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), R.kp, R.n, cap,
                                     ctx->kp.as<Keypoint>(), ctx->stream));
-    HIPCHK(launch_count_keypoints(ctx->pos.as<unsigned>(), ctx->keep.as<unsigned>(), R.n, cap, cnt + kCntKp, ctx->stream));
+    HIPCHK(launch_count_keypoints(P, ctx->pos.as<unsigned>(), ctx->keep.as<unsigned>(), R.cand_key, R.n, cap,
+                                  cnt + kCntKp, cnt + kBlk, ctx->stream));
     if (ctx->p.flags & SIFT_F_KEYPOINT_ORIGINS) {
       HIPCHK(ctx->kp_key.ensure((size_t)cap * sizeof(unsigned)));
       HIPCHK(launch_scatter_keys(ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), R.cand_key, R.n, cap,

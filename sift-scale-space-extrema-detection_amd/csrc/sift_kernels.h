@@ -159,15 +159,24 @@ hipError_t launch_scatter_keypoints(const unsigned* keep, const unsigned* pos, c
                                     const unsigned* n, int cap, Keypoint* out, hipStream_t st);
 // keep[i] = status[i] is a kept keypoint whose candidate row (whole-image
 // octave rows, P.row0 applied) lies in the input rows [own_lo, own_hi) (own_lo
-// < 0: every row; own_hi < 0: no upper bound); blk[o * S + s - 1] counts them
-// per (octave, scale).
+// < 0: every row; own_hi < 0: no upper bound).  blk (kBlkWords, zeroed by the
+// caller) receives the first slot of every (octave, scale) block of the
+// candidate list at blk[kBlkStart + b], b = o * S + s - 1 (candidates are in
+// key order, so a block is a slot range), or sets blk[kBlkUnsorted] when the
+// list is not in key order.
+constexpr int kBlkN = kMaxOctaves * kMaxScales;   // blk[b]: kept keypoints of block b (launch_count_keypoints)
+constexpr int kBlkStart = kBlkN;                  // blk[kBlkStart + b], b <= O*S: first slot of block b
+constexpr int kBlkUnsorted = kBlkStart + kBlkN + 1;
+constexpr int kBlkWords = kBlkUnsorted + 1;
 hipError_t launch_status_to_keep(const Pyramid& P, const int* status, const unsigned* key, unsigned* keep,
                                  const unsigned* n, int cap, int own_lo, int own_hi, unsigned* blk, hipStream_t st);
 hipError_t launch_scatter_keys(const unsigned* keep, const unsigned* pos, const unsigned* key, const unsigned* n,
                                int cap, unsigned* out, hipStream_t st);
-// out = pos[n-1] + keep[n-1] (0 if n == 0): the number of keypoints.
-hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, const unsigned* n, int cap,
-                                  unsigned* out, hipStream_t st);
+// out = pos[n-1] + keep[n-1] (0 if n == 0): the number of keypoints; blk[b] =
+// kept keypoints of block b, from the block starts and the exclusive scan pos
+// (a histogram over the slots when the list was not in key order).
+hipError_t launch_count_keypoints(const Pyramid& P, const unsigned* pos, const unsigned* keep, const unsigned* key,
+                                  const unsigned* n, int cap, unsigned* out, unsigned* blk, hipStream_t st);
 
 size_t exact_lds_bytes(const Pyramid& P);
 

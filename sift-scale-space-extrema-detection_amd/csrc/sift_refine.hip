@@ -423,38 +423,41 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
   }
 }
 
+__device__ __forceinline__ int key_block(const Pyramid& P, unsigned key) {
+  int o, s, y, x;
+  decode_key(P, key, o, s, y, x);
+  return o * P.S + (s - 1);
+}
+
 __global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const int* __restrict__ status,
                                                         const unsigned* __restrict__ key,
                                                         unsigned* __restrict__ keep, const unsigned* __restrict__ n,
                                                         int cap, int own_lo, int own_hi,
                                                         unsigned* __restrict__ blk) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  int b = -1;  // (octave, scale) block of a kept keypoint
-  if (i < cap) {
-    bool k = i < (int)min(*n, (unsigned)cap) && status[i] == kRefKeep;
-    if (k) {
-      int o, s, y, x;
-      decode_key(P, key[i], o, s, y, x);
-      if (own_lo >= 0) {  // row-band ownership by candidate row (octave o rows: 2 r at o = 0, r >> (o-1))
-        const int yw = y + ((P.row0 * 2) >> o);
-        const int lo = o == 0 ? 2 * own_lo : own_lo >> (o - 1);
-        const int hi = own_hi < 0 ? 0x7fffffff : (o == 0 ? 2 * own_hi : own_hi >> (o - 1));
-        k = yw >= lo && yw < hi;
-      }
-      if (k) b = o * P.S + (s - 1);
+  if (i >= cap) return;
+  const int m = (int)min(*n, (unsigned)cap);
+  bool k = false;
+  if (i < m) {
+    int o, s, y, x;
+    decode_key(P, key[i], o, s, y, x);
+    const int b = o * P.S + (s - 1), nb = P.O * P.S;
+    k = status[i] == kRefKeep;
+    if (k && own_lo >= 0) {  // row-band ownership by candidate row (octave o rows: 2 r at o = 0, r >> (o-1))
+      const int yw = y + ((P.row0 * 2) >> o);
+      const int lo = o == 0 ? 2 * own_lo : own_lo >> (o - 1);
+      const int hi = own_hi < 0 ? 0x7fffffff : (o == 0 ? 2 * own_hi : own_hi >> (o - 1));
+      k = yw >= lo && yw < hi;
     }
-    keep[i] = k ? 1u : 0u;
+    // block starts: slot i opens blocks (block(i-1), block(i)]; no atomics (a
+    // per-block counter would serialise ~10^4 same-address atomics)
+    const int bp = i == 0 ? -1 : key_block(P, key[i - 1]);
+    if (b < bp) blk[kBlkUnsorted] = 1u;
+    for (int q = bp + 1; q <= b; ++q) blk[kBlkStart + q] = (unsigned)i;
+    if (i == m - 1)
+      for (int q = max(b, bp) + 1; q <= nb; ++q) blk[kBlkStart + q] = (unsigned)m;
   }
-  // per-block counts, one atomic per distinct block of the wave (keys are sorted)
-  for (;;) {
-    const unsigned long long act = __ballot(b >= 0);
-    if (!act) break;
-    const int lead = __ffsll((long long)act) - 1;
-    const int first = __shfl(b, lead);
-    const unsigned long long same = __ballot(b == first);
-    if ((int)(threadIdx.x & 63) == lead) atomicAdd(&blk[first], (unsigned)__popcll(same));
-    if (b == first) b = -1;
-  }
+  keep[i] = k ? 1u : 0u;
 }
 
 // keep: k_status_to_keep's flags (kept keypoint, in the owned rows).
@@ -478,10 +481,27 @@ __global__ __launch_bounds__(256) void k_scatter_key(const unsigned* __restrict_
   if (i < cap && i < (int)min(*n, (unsigned)cap) && keep[i]) out[pos[i]] = key[i];
 }
 
-__global__ void k_count_kp(const unsigned* __restrict__ pos, const unsigned* __restrict__ keep,
-                           const unsigned* __restrict__ n, unsigned cap, unsigned* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_count_kp(const Pyramid P, const unsigned* __restrict__ pos,
+                                                  const unsigned* __restrict__ keep, const unsigned* __restrict__ key,
+                                                  const unsigned* __restrict__ n, unsigned cap,
+                                                  unsigned* __restrict__ out, unsigned* __restrict__ blk) {
+  __shared__ unsigned hist[kBlkN];
   const unsigned m = min(*n, cap);
-  *out = m ? pos[m - 1] + keep[m - 1] : 0u;
+  const int nb = P.O * P.S;
+  auto kept_before = [&](unsigned j) { return j < cap ? pos[j] : pos[cap - 1] + keep[cap - 1]; };
+  if (threadIdx.x == 0) *out = m ? kept_before(m) : 0u;
+  if (!m) return;  // blk[b] stays 0
+  if (!blk[kBlkUnsorted]) {
+    for (int b = threadIdx.x; b < nb; b += blockDim.x)
+      blk[b] = kept_before(blk[kBlkStart + b + 1]) - kept_before(blk[kBlkStart + b]);
+    return;
+  }
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  for (unsigned i = threadIdx.x; i < m; i += blockDim.x)
+    if (keep[i]) atomicAdd(&hist[key_block(P, key[i])], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) blk[b] = hist[b];
 }
 
 // Candidate key of each keypoint -> (octave, scale, whole-image row, x).
@@ -568,9 +588,10 @@ hipError_t launch_scatter_keys(const unsigned* keep, const unsigned* pos, const 
   return hipGetLastError();
 }
 
-hipError_t launch_count_keypoints(const unsigned* pos, const unsigned* keep, const unsigned* n, int cap,
-                                  unsigned* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_count_kp, dim3(1), dim3(1), 0, st, pos, keep, n, (unsigned)cap, out);
+hipError_t launch_count_keypoints(const Pyramid& P, const unsigned* pos, const unsigned* keep, const unsigned* key,
+                                  const unsigned* n, int cap, unsigned* out, unsigned* blk, hipStream_t st) {
+  if (cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_count_kp, dim3(1), dim3(256), 0, st, P, pos, keep, key, n, (unsigned)cap, out, blk);
   return hipGetLastError();
 }
 

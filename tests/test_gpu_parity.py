@@ -408,6 +408,31 @@ def test_keypoint_origins_and_next_seed(gpu_ctx):
     np.testing.assert_array_equal(seed.astype(np.float32), gpu_ctx.plane(sift_amd.PLANE_GAUSS, 3, 0))
 
 
+def test_block_counts_of_caller_candidates_in_any_order(gpu_ctx):
+    """Per-block counts come from the block starts of a key-ordered list; a
+    caller list out of key order (sift_set_candidates) takes the histogram
+    path and still counts every kept keypoint in its block."""
+    img = blob_image(320, 240, seed=19)
+    O, S = 4, 3
+    p = sift_amd.make_params(O, S, flags=sift_amd.F_KEYPOINT_ORIGINS)
+    gpu_ctx.build_scale_space(img, p)
+    cand, _ = gpu_ctx.find_extrema()
+    kp_sorted, _ = gpu_ctx.refine()
+    org = gpu_ctx.keypoint_origins()  # blocks are by candidate (octave, scale)
+    want = np.bincount(org[:, 0] * S + org[:, 1] - 1, minlength=O * S)
+    assert want.sum() == kp_sorted.shape[0] > 0
+    np.testing.assert_array_equal(gpu_ctx.block_counts(), want)
+    rev = cand[::-1].copy()
+    gpu_ctx.set_candidates(rev)
+    kp_rev, _ = gpu_ctx.refine()
+    assert kp_rev.shape == kp_sorted.shape
+    np.testing.assert_array_equal(gpu_ctx.block_counts(), want)
+    gpu_ctx.set_candidates(cand[:1].copy())
+    kp1, _ = gpu_ctx.refine()
+    got = gpu_ctx.block_counts()
+    assert got.sum() == kp1.shape[0] <= 1
+
+
 def test_owned_rows_and_block_counts(gpu_ctx):
     """sift_set_owned_rows keeps exactly the keypoints whose candidate row lies
     in the band (octave rows 2 r at octave 0, r >> (o-1) above); the per-block
