@@ -105,6 +105,7 @@ struct sift_ctx {
   DBuf img, seeds, gauss, dog, wts;
   DBuf base0;                                  // materialised octave-0 base (large radii only)
   DBuf l64;                                    // fp64 Gaussian planes of the large-radius octaves
+  DBuf vsplit;                                 // vertical-sum scratch of the split-pass octaves (one at a time)
   std::vector<double> wts_host;                // taps last uploaded to wts
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
@@ -259,7 +260,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->l64, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
+  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->l64, &ctx->vsplit, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->xseed, &ctx->kp_key, &ctx->counters,
@@ -465,6 +466,10 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
       }
     if (l64) HIPCHK(ctx->l64.ensure((size_t)l64 * sizeof(double)));
     P.l64 = l64 ? ctx->l64.as<double>() : nullptr;
+    size_t vs = 0;  // the split-pass octaves run in turn on this stream: one scratch
+    for (int o = o_first; o < P.O; ++o)
+      if (gauss_vsplit(P, o)) vs = std::max(vs, (size_t)P.NS * P.oct[o].h * P.oct[o].w);
+    if (vs) HIPCHK(ctx->vsplit.ensure(vs * sizeof(double)));
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   const double* base0 = nullptr;
@@ -526,6 +531,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
       ls = ctx->hi;
     }
     L.l64 = P.oct[o].l64_off >= 0 ? ctx->l64.as<double>() + P.oct[o].l64_off : nullptr;
+    L.vsplit = gauss_vsplit(P, o) ? ctx->vsplit.as<double>() : nullptr;
     HIPCHK(launch_gauss_dog(P, L, ls));
     if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ls));
     HIPCHK(hipEventRecord(ctx->ev_go[o], ls));

@@ -238,6 +238,71 @@ __device__ __forceinline__ void vert_glob_gen(const GTile& T, int r, const cdoub
 }
 
 // ---------------------------------------------------------------------------
+// Split vertical pass (large radii, gauss_vsplit).  A 64-column tile
+// recomputes the vertical sums of its 2r halo columns: (64 + 2r) / 64 of the
+// vertical work (2.5x at r = 47, 6.9x at r = 188), serialised in the tile's
+// waves.  k_gauss_vert computes every (scale, row, column) sum once, one lane
+// per column and eight rows per wave, into fp64 scratch planes, with
+// vert_glob_gen's exact chunking (rows yb + jb + k, zero-padded taps in
+// increasing order from 0.0): every value is bit-identical to the tile
+// kernel's own.  The tile kernel then copies its strip (vert_copy).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gauss_vert(const Pyramid P, int o, const double* __restrict__ base,
+                                                    double* __restrict__ vout) {
+  const Octave& oc = P.oct[o];
+  const int s = blockIdx.z;
+  const int r = oc.rad[s], h = oc.h, w = oc.w;
+  const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int x = blockIdx.x * kGX + lane;
+  const int y0 = blockIdx.y * kGY + 8 * wv;
+  if (y0 >= h) return;  // wave-uniform
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, h * w * 8,
+                                                                      0x00020000);
+  const int xoff = min(x, w - 1) * 8;
+  const int NJ = 2 * r + 8, yb = y0 - r;
+  double acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+  for (int jb = 0; jb < NJ; jb += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      v[k] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, h - 1) * w * 8));
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = fma((double)wp[jb + k - t], v[k], acc[t]);  // zero-padded taps
+    pin(acc);
+  }
+  if (x < w) {
+    double* dst = vout + (long long)s * h * w + (long long)y0 * w + x;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (y0 + t < h) dst[(long long)t * w] = acc[t];
+  }
+}
+
+// The wave's 8 strip rows, columns x0 - r .. x0 + 63 + r (clamped), from the
+// split pass's plane of this scale; rows past the plane (outputs dropped)
+// read its last row.
+__device__ __forceinline__ void vert_copy(const GTile& T, int r, const double* __restrict__ src, double* V) {
+  const int NC = kGX + 2 * r;
+  double* Vw = V + 8 * T.wv * T.sw;
+  const int yr = T.y0 + 8 * T.wv;
+  for (int cb = 0; cb < NC; cb += 64) {
+    const int c = cb + T.lane;
+    const int xo = clampi(T.x0 - r + min(c, NC - 1), 0, T.w - 1);
+    double v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = src[(long long)min(yr + t, T.h - 1) * T.w + xo];
+    if (c < NC)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) Vw[t * T.sw + c] = v[t];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Vertical pass, octave 0, staged input region: input column kb + c (kb =
 // x0/2 - ceil(r/2)), output rows e + t (e = y0 + 8 wv, even).  Tap k of
 // output row e + t reads input row e/2 + floor((t + k - r)/2), i.e. window
@@ -618,7 +683,12 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     // keeps it all live (dozens of VGPRs, half the occupancy).
     GTile Ts = T;
     asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
-    vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
+    if constexpr (!OCT0) {
+      if (L.vsplit) vert_copy(Ts, oc.rad[s], L.vsplit + (long long)s * plane, V);
+      else vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
+    } else {
+      vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
+    }
     wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
     double out[kNR][4];
     horz_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V, out);
@@ -733,6 +803,13 @@ bool gauss_needs_base0(const Pyramid& P) { return P.oct[0].rmax > kUR; }
 // S=5: octaves 4 and 5; at 4K octave 3, radius 47, it measured slower: 0.71 -> 0.74 ms pass).
 bool gauss_keep_l64(const Pyramid& P, int o) {
   static const int rmin = [] { const char* e = std::getenv("SIFT_L64_R"); return e ? std::atoi(e) : 90; }();
+  return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin;
+}
+
+// Octaves o >= 1 whose largest radius reaches SIFT_VSPLIT_R (default 40; 0 =
+// never) run the split vertical pass (k_gauss_vert) before the tile kernel.
+bool gauss_vsplit(const Pyramid& P, int o) {
+  static const int rmin = [] { const char* e = std::getenv("SIFT_VSPLIT_R"); return e ? std::atoi(e) : 40; }();
   return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin;
 }
 
@@ -880,6 +957,11 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
                    (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
   L.vec = (a16 && (oc.w & 3) == 0 && 4.0 * oc.h * oc.w < 2147483648.0) ? 1 : 0;
   L.zero = oc.rmax > (staged0(P, L.o) ? kUR : kUR1) ? 1 : 0;
+  if (L.vsplit) {
+    if (L.o == 0 || !L.base) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_gauss_vert, dim3((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, P.NS), dim3(256), 0, st, P,
+                       L.o, L.base, L.vsplit);
+  }
   if (L.fuse) {  // staged octave 0 (gauss_can_fuse)
     if (L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, true>), grid, dim3(256), lds, st, P, L);
     else hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, true>), grid, dim3(256), lds, st, P, L);

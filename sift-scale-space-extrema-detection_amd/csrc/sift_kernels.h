@@ -41,6 +41,8 @@ struct GaussLaunch {
   int next_w;
   const double* base; // fp64 octave base h x w (o >= 1: the seed; o == 0: only when materialised)
   double* l64;        // plane (o, 0) of the kept fp64 Gaussian planes, nullptr = not kept
+  double* vsplit;     // large radii (gauss_vsplit): fp64 scratch of NS vertical-sum planes h x w, filled by a
+                      // separate launch; the tile kernel copies its strip from it (nullptr = one pass)
   // filled by launch_gauss_dog
   int sw;             // strip row stride (doubles)
   int vec;            // float4 plane stores are aligned
@@ -140,6 +142,10 @@ hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int 
 // Octave o stores its fp64 Gaussian planes too (GaussLaunch.l64): the exact
 // passes then read the patch values instead of recomputing them.
 bool gauss_keep_l64(const Pyramid& P, int o);
+
+// Octave o runs the split vertical pass (GaussLaunch.vsplit scratch: NS x h x
+// w doubles).
+bool gauss_vsplit(const Pyramid& P, int o);
 
 // Fills the unit table of L (octave geometry) and launches the scan; returns
 // the launch error.  L.bitmap words per octave: S * h * nw.
