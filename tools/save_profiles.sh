@@ -15,6 +15,6 @@ cp $G/bench_${T}.json $P/${T}_bench.json
 cp $G/bench_prof_${T}.json $P/${T}_bench_under_rocprof.json
 cp $G/bench_prof_${T}_iso.json $P/${T}_iso_bench_under_rocprof.json
 python3 $R/tools/gauss_oct.py $G/prof_${T}_iso/run_kernel_trace.csv $G/prof_${T}/run_kernel_trace.csv > $P/${T}_per_octave_trace.txt
-cp $G/pytest_gpu_${T}.log $P/${T}_pytest_gpu.log
+[ -f $G/pytest_gpu_${T}.log ] && cp $G/pytest_gpu_${T}.log $P/${T}_pytest_gpu.log
 cp $G/smoke_${T}.log $P/${T}_smoke.log
 echo saved $T
