@@ -461,8 +461,8 @@ def gather_rows(t, counts, group=None):
 def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, timer=None):
     """One shard per rank, device-resident (RCCL with the nccl backend).
     Rank r runs its row band (octaves 0..K, keypoints of its own rows), the
-    owned rows of the octave-(K+1) base are all-gathered, tail octave K+1+j is
-    detected by rank j (round robin), then the per-(octave, scale) counts and
+    owned rows of the octave-(K+1) base are all-gathered, every tail octave is
+    detected by one rank (tail_octaves: the deepest on the smallest crops), then the per-(octave, scale) counts and
     the keypoints are all-gathered and merged block-major (no sort).  Every
     rank returns the whole image's keypoints (uint8 [n, 48] on its device) in
     the reference's order."""
