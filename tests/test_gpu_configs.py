@@ -153,3 +153,34 @@ def test_fused_extrema_flag_same_results(gpu_ctx, W, H, O, S, seed):
     cb, nb = gpu_ctx.candidates(), gpu_ctx.counts()
     assert a.tobytes() == b.tobytes() and ca.tobytes() == cb.tobytes()
     assert na["low_contrast"] == nb["low_contrast"] and na["candidates"] == nb["candidates"]
+
+
+@pytest.mark.timeout(300)
+def test_capacity_growth_on_dense_extrema():
+    """A fresh context starts from a geometry estimate of its candidate,
+    ambiguous-key and low-contrast capacities; a noisy 3-pixel
+    dot lattice image has more extrema than that estimate (1 per 9 input
+    pixels at every scale), so the extrema stage overflows, grows and runs again (the
+    retry path), and the results still equal the oracle's in the HIP path's
+    operation order.  A second detection on the grown context runs without
+    a retry and gives the same bytes."""
+    rng = np.random.default_rng(5)
+    H, W = 960, 1280
+    y, x = np.mgrid[0:H, 0:W]
+    img = (0.5 + 0.4 * ((x % 3 == 1) & (y % 3 == 1)) + 0.01 * rng.random((H, W))).astype(np.float32)
+    ctx = sift_amd.Context(0)
+    try:
+        p = sift_amd.make_params(3, 3, flags=sift_amd.F_LOW_CONTRAST_LIST)
+        kp = ctx.detect(img, p).copy()
+        cand, low, counts = ctx.candidates(), ctx.low_contrast(), ctx.counts()
+        r = orc.OracleRun(img, oracle_params(p), orc.CONV_SEPARABLE_FMA_VH, threads=host_threads())
+        print("\ndot lattice 1280x960 O3 S3: %d candidates, %d low, %d keypoints, %d exact re-decisions"
+              % (cand.shape[0], low.shape[0], kp.shape[0], counts["exact"]))
+        assert cand.shape[0] > 3 * 6451200 // 192  # above the initial estimate: the retry ran
+        check_candidates(cand, r.candidates())
+        check_candidates(low, r.low_contrast())
+        check_keypoints(kp, r.refined)
+        again = ctx.detect(img, p).copy()
+        assert again.tobytes() == kp.tobytes()
+    finally:
+        ctx.close()
