@@ -59,7 +59,7 @@ constexpr int kGX = 64;              // tile columns
 constexpr int kGY = 32;              // tile rows: 4 waves x 8
 constexpr int kUR = 16;              // radii with unrolled code (octave 0)
 #ifndef SIFT_UR1
-#define SIFT_UR1 8
+#define SIFT_UR1 12
 #endif
 #ifndef SIFT_STORE_AUX
 #define SIFT_STORE_AUX 18 // cache-policy bits of the plane stores (gfx950: 1 sc0, 2 nt, 16 sc1)
