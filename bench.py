@@ -215,7 +215,9 @@ def main():
     from sift_amd.synth import blob_image
 
     dist = None
-    if world > 1:
+    # SIFT_BENCH_DIST=1: the collective path at world size 1 too (rehearsal of
+    # the N > 1 code on a one-GPU box under torchrun)
+    if world > 1 or os.environ.get("SIFT_BENCH_DIST") == "1":
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")  # RCCL over xGMI
@@ -239,8 +241,11 @@ def main():
 
     gather = None
     if dist is not None:
-        from sift_amd.dist import KeypointGather
-        gather = KeypointGather("cuda:%d" % dev)
+        # every image's keypoint list reaches every rank (RCCL all-gather over
+        # xGMI); the records gather is left in flight under the next images'
+        # detections (the counts gather is the step's only synchronisation)
+        from sift_amd.dist import PipelinedKeypointGather
+        gather = PipelinedKeypointGather("cuda:%d" % dev, depth=nin)
 
     stage = {"gauss_dog_ms": 0.0, "extrema_ms": 0.0, "refine_ms": 0.0, "gauss_oct0_ms": 0.0}
     oct_ms = [0.0] * O
@@ -306,6 +311,8 @@ def main():
     flush()
     for i in range(max(0, NI - (nin - 1)), NI):
         n_total = finish(i, True)
+    if gather is not None:
+        gather.drain()  # the last records gathers complete inside the timed region
     for c in ctxs:
         c.synchronize()
     torch.cuda.synchronize(dev)

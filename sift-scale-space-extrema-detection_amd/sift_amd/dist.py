@@ -68,6 +68,69 @@ class KeypointGather:
         return np.concatenate(parts) if parts else np.zeros(0, dtype=KEYPOINT_DTYPE)
 
 
+class PipelinedKeypointGather:
+    """The same all-gather, overlapped with the detections that follow.
+
+    Per step the counts are all-gathered synchronously (8 B per rank), then
+    the records all-gather is only enqueued (async_op) and this step's
+    buffers are left to it; a ring of `depth` send / receive buffers keeps
+    `depth - 1` record gathers in flight while the GPU keeps detecting.  A
+    slot is reused only after its gather has completed on the device and the
+    host has seen that (the next fill writes the send buffer from another HIP
+    runtime's stream, which nothing else orders after RCCL's).  `drain()`
+    completes every outstanding gather; `gathered(k)` is the host view of the
+    step k slots back (after drain)."""
+
+    def __init__(self, device, group=None, depth=3):
+        self.device = torch.device(device)
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.depth = max(1, int(depth))
+        self.slots = [{"cap": 0, "send": None, "recv": None, "work": None, "counts": None}
+                      for _ in range(self.depth)]
+        self.k = 0
+
+    def _settle(self, slot):
+        if slot["work"] is not None:
+            slot["work"].wait()
+            if self.device.type == "cuda":
+                torch.cuda.current_stream(self.device).synchronize()
+            slot["work"] = None
+
+    def __call__(self, n_local, fill):
+        cnt = torch.tensor([int(n_local)], dtype=torch.int64, device=self.device)
+        cnts = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(cnts, cnt, group=self.group)
+        counts = [int(c) for c in cnts.tolist()]
+        slot = self.slots[self.k % self.depth]
+        self.k += 1
+        self._settle(slot)
+        need = max(max(counts), 1)
+        if need > slot["cap"]:
+            cap = need + need // 4
+            slot["send"] = torch.zeros(cap * REC, dtype=torch.uint8, device=self.device)
+            slot["recv"] = torch.zeros(self.world * cap * REC, dtype=torch.uint8, device=self.device)
+            slot["cap"] = cap
+        n = fill(slot["send"], slot["cap"])
+        assert n == n_local, (n, n_local)
+        slot["work"] = dist.all_gather_into_tensor(slot["recv"], slot["send"], group=self.group, async_op=True)
+        slot["counts"] = counts
+        return counts
+
+    def drain(self):
+        for slot in self.slots:
+            self._settle(slot)
+
+    def gathered(self, back=1):
+        """Host view of the step `back` steps ago (1 = the last), rank order."""
+        slot = self.slots[(self.k - back) % self.depth]
+        self._settle(slot)
+        counts, cap = slot["counts"], slot["cap"]
+        raw = slot["recv"].view(self.world, cap * REC).cpu().numpy()
+        parts = [np.frombuffer(raw[r, :counts[r] * REC].tobytes(), dtype=KEYPOINT_DTYPE) for r in range(self.world)]
+        return np.concatenate(parts) if parts else np.zeros(0, dtype=KEYPOINT_DTYPE)
+
+
 def host_fill(records):
     """fill() for host-side keypoint arrays (tests / CPU ranks)."""
     raw = np.ascontiguousarray(records, dtype=KEYPOINT_DTYPE).view(np.uint8)

@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from sift_amd import KEYPOINT_DTYPE
-from sift_amd.dist import KeypointGather, host_fill, shard_images
+from sift_amd.dist import KeypointGather, PipelinedKeypointGather, host_fill, shard_images
 
 
 def _free_port():
@@ -47,6 +47,17 @@ def _worker(rank, world, port, counts, out_q):
             mine = fake_keypoints(rank, per_rank[rank])
             c = g(mine.shape[0], host_fill(mine))
             res.append((c, g.gathered(c).tobytes()))
+        # the pipelined form: gathers left in flight over a ring of 2 slots, read back a step later
+        pg = PipelinedKeypointGather("cpu", depth=2)
+        pres = []
+        for step, per_rank in enumerate(counts):
+            mine = fake_keypoints(rank, per_rank[rank])
+            c = pg(mine.shape[0], host_fill(mine))
+            if step:
+                pres.append(pg.gathered(2).tobytes())
+        pg.drain()
+        pres.append(pg.gathered(1).tobytes())
+        res.append(pres)
         out_q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -72,6 +83,7 @@ def test_keypoint_all_gather_matches_concatenation(world):
             assert c == per_rank
             got = np.frombuffer(blob, dtype=KEYPOINT_DTYPE)
             assert got.tobytes() == expect.tobytes()
+            assert results[r][len(counts)][step] == expect.tobytes()  # pipelined, one step later
 
 
 def test_shard_images_covers_batch_once():

@@ -52,6 +52,24 @@ def test_keypoint_gather_over_rccl_from_library_buffer(gpu_ctx, nccl_world1):
         assert g.gathered(counts).tobytes() == want.tobytes()
 
 
+def test_pipelined_keypoint_gather_over_rccl(gpu_ctx, nccl_world1):
+    """bench.py's gather: records all-gathers left in flight over a ring of
+    slots while the next detections run, read back after drain()."""
+    import torch
+    from sift_amd.dist import PipelinedKeypointGather
+    p = sift_amd.make_params(4, 3)
+    imgs = [blob_image(480 + 32 * k, 360, seed=40 + k) for k in range(4)]
+    want = [gpu_ctx.detect(im, p).copy() for im in imgs]
+    g = PipelinedKeypointGather("cuda:0", depth=3)
+    for im in imgs:
+        d = torch.from_numpy(im).to("cuda:0")
+        n = gpu_ctx.detect_device(d.data_ptr(), im.shape[1], im.shape[0], p)
+        g(n, lambda buf, cap: gpu_ctx.copy_keypoints_device(buf.data_ptr(), cap))
+    g.drain()
+    for back in (1, 2, 3):
+        assert g.gathered(back).tobytes() == want[len(imgs) - back].tobytes()
+
+
 @pytest.mark.parametrize("W,H,O,S", [(1280, 720, 5, 4), (640, 480, 6, 3)])
 def test_row_band_driver_over_rccl_equals_whole_image(gpu_ctx, nccl_world1, W, H, O, S):
     import torch
