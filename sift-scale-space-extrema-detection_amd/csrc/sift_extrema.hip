@@ -188,8 +188,12 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
 // is reduced once (3-wide max/min with DPP shifts) and shared by the scales
 // above and below it; the decisions are SALU lane-mask logic.
 // LOWL: also the bitmap of the certain low-contrast extrema (their list).
+#ifndef SIFT_XMINW
+#define SIFT_XMINW 1  // minimum waves per SIMD of the scan (register budget; experiments)
+#endif
+
 template <bool LOWL>
-__global__ __launch_bounds__(256) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
+__global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
   const int u = L.u_begin + (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (u >= L.u_end) return;
   int o = 0;
