@@ -1425,39 +1425,46 @@ int sift_detect_from_seed_range_device(sift_ctx* ctx, int octave_first, int octa
 int sift_merge_keypoint_blocks_device(sift_ctx* ctx, const sift_keypoint* d_in, const int64_t* counts, int n_parts,
                                       int n_blocks, sift_keypoint* d_out) {
   if (!ctx || !counts || n_parts < 1 || n_blocks < 1 || n_parts > 1024 || n_blocks > 4096) return SIFT_E_ARG;
-  // tab: part_start[np + 1] | in_start[np][nb + 1] | out_off[nb][np]
+  // Every (part, block) run is contiguous in d_in and in d_out: the merge is
+  // one copy per non-empty run (seg = src, dst, bytes; cstart = first chunk).
   const int np = n_parts, nb = n_blocks;
-  std::vector<long long> tab((size_t)(np + 1) + (size_t)np * (nb + 1) + (size_t)nb * np);
-  long long* part_start = tab.data();
-  long long* in_start = part_start + np + 1;
-  long long* out_off = in_start + (size_t)np * (nb + 1);
-  long long n = 0;
+  constexpr long long kRec = sizeof(sift_keypoint), kChunk = kMergeChunk;
+  std::vector<long long> part_start((size_t)np + 1, 0);
   for (int q = 0; q < np; ++q) {
-    part_start[q] = n;
     long long a = 0;
     for (int b = 0; b < nb; ++b) {
       const long long c = counts[(size_t)q * nb + b];
       if (c < 0) return set_err(ctx, SIFT_E_ARG, "negative count");
-      in_start[(size_t)q * (nb + 1) + b] = a;
       a += c;
     }
-    in_start[(size_t)q * (nb + 1) + nb] = a;
-    n += a;
+    part_start[q + 1] = part_start[q] + a;
   }
-  part_start[np] = n;
-  long long o = 0;
+  std::vector<long long> in_at(part_start.begin(), part_start.end() - 1);  // next record of each part
+  std::vector<long long> seg, cstart;
+  long long o = 0, chunks = 0;
   for (int b = 0; b < nb; ++b)
     for (int q = 0; q < np; ++q) {
-      out_off[(size_t)b * np + q] = o;
-      o += counts[(size_t)q * nb + b];
+      const long long c = counts[(size_t)q * nb + b];
+      if (!c) continue;
+      seg.push_back(in_at[q] * kRec);
+      seg.push_back(o * kRec);
+      seg.push_back(c * kRec);
+      cstart.push_back(chunks);
+      chunks += (c * kRec + kChunk - 1) / kChunk;
+      in_at[q] += c;
+      o += c;
     }
-  if (n == 0) return SIFT_OK;
+  if (o == 0) return SIFT_OK;
   if (!d_in || !d_out) return SIFT_E_ARG;
+  const int nseg = (int)cstart.size();
+  std::vector<long long> tab(seg);
+  tab.insert(tab.end(), cstart.begin(), cstart.end());
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(ctx->merge_tab.ensure(tab.size() * sizeof(long long)));
   HIPCHK(hipMemcpyAsync(ctx->merge_tab.p, tab.data(), tab.size() * sizeof(long long), hipMemcpyHostToDevice,
                         ctx->stream));
-  HIPCHK(launch_merge_blocks(reinterpret_cast<const Keypoint*>(d_in), n, ctx->merge_tab.as<long long>(), np, nb,
+  HIPCHK(launch_merge_blocks(reinterpret_cast<const Keypoint*>(d_in), ctx->merge_tab.as<long long>(),
+                             ctx->merge_tab.as<long long>() + 3 * (size_t)nseg, nseg, chunks,
                              reinterpret_cast<Keypoint*>(d_out), ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return SIFT_OK;

@@ -186,10 +186,13 @@ hipError_t launch_count_keypoints(const Pyramid& P, const unsigned* pos, const u
 
 size_t exact_lds_bytes(const Pyramid& P);
 
-// Block-major merge of n keypoints in np parts (sift_merge_keypoint_blocks_device):
-// tab = part_start[np + 1] | in_start[np][nb + 1] | out_off[nb][np] (device).
-hipError_t launch_merge_blocks(const Keypoint* in, long long n, const long long* tab, int np, int nb, Keypoint* out,
-                               hipStream_t st);
+// Block-major merge (sift_merge_keypoint_blocks_device) as copies of the
+// nseg contiguous (part, block) runs: seg[3 i] = {source byte offset,
+// destination byte offset, bytes}, cstart[i] = first 16-KiB chunk of run i,
+// n_chunks = cstart[nseg] (device tables).
+constexpr long long kMergeChunk = 16384;
+hipError_t launch_merge_blocks(const Keypoint* in, const long long* seg, const long long* cstart, int nseg,
+                               long long n_chunks, Keypoint* out, hipStream_t st);
 
 // keys -> 4 int32 per keypoint: octave, scale, whole-image octave row (row0 applied), x.
 hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st);

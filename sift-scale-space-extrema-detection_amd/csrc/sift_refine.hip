@@ -517,32 +517,36 @@ __global__ __launch_bounds__(256) void k_decode_origins(const Pyramid P, const u
   out[4 * i + 3] = x;
 }
 
-// One thread per keypoint: its part (linear, np small), its block (binary
-// search of the part's block starts), its place in the block-major output.
-__global__ __launch_bounds__(256) void k_merge_blocks(const Keypoint* __restrict__ in, long long n,
-                                                      const long long* __restrict__ tab, int np, int nb,
-                                                      Keypoint* __restrict__ out) {
-  const long long i = blockIdx.x * 256LL + threadIdx.x;
-  if (i >= n) return;
-  const long long* part_start = tab;
-  const long long* in_start = tab + np + 1;
-  const long long* out_off = in_start + (long long)np * (nb + 1);
-  int p = 0;
-  while (p + 1 < np && i >= part_start[p + 1]) ++p;
-  const long long local = i - part_start[p];
-  const long long* st = in_start + (long long)p * (nb + 1);
-  int lo = 0, hi = nb - 1;  // largest b with st[b] <= local (empty blocks: st[b] == st[b+1])
+// Block-major merge as segment copies: every (part, block) run of keypoints
+// is contiguous in the input and in the output, so one workgroup copies one
+// 16-KiB chunk of one run with 16-byte loads and stores (records are 48 B).
+// seg[3 i] = {source byte offset, destination byte offset, bytes} of run i;
+// cstart[i] = its first chunk (the grid is cstart[nseg]).
+
+__global__ __launch_bounds__(256) void k_merge_blocks(const unsigned char* __restrict__ in,
+                                                      unsigned char* __restrict__ out,
+                                                      const long long* __restrict__ seg,
+                                                      const long long* __restrict__ cstart, int nseg) {
+  const long long c = blockIdx.x;
+  int lo = 0, hi = nseg - 1;  // the run of chunk c: the last with cstart <= c
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (st[mid] <= local) lo = mid; else hi = mid - 1;
+    if (cstart[mid] <= c) lo = mid; else hi = mid - 1;
   }
-  out[out_off[(long long)lo * np + p] + (local - st[lo])] = in[i];
+  const long long* sg = seg + 3 * (long long)lo;
+  const long long off = (c - cstart[lo]) * kMergeChunk;
+  const long long n16 = min(kMergeChunk, sg[2] - off) >> 4;
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(in + sg[0] + off);
+  uint4* __restrict__ dst = reinterpret_cast<uint4*>(out + sg[1] + off);
+  for (long long i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
 }
 
-hipError_t launch_merge_blocks(const Keypoint* in, long long n, const long long* tab, int np, int nb, Keypoint* out,
-                               hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, tab, np, nb, out);
+hipError_t launch_merge_blocks(const Keypoint* in, const long long* seg, const long long* cstart, int nseg,
+                               long long n_chunks, Keypoint* out, hipStream_t st) {
+  if (nseg <= 0 || n_chunks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge_blocks, dim3((unsigned)n_chunks), dim3(256), 0, st,
+                     reinterpret_cast<const unsigned char*>(in), reinterpret_cast<unsigned char*>(out), seg, cstart,
+                     nseg);
   return hipGetLastError();
 }
 
