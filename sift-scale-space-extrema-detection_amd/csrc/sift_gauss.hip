@@ -67,6 +67,17 @@ constexpr int kUR = 16;              // radii with unrolled code (octave 0)
 #ifndef SIFT_MINW1
 #define SIFT_MINW1 1
 #endif
+#ifndef SIFT_VERT2
+#define SIFT_VERT2 1  // octaves >= 1: two columns per lane, 16-byte loads (vert_glob2)
+#endif
+#ifndef SIFT_V2PF
+#define SIFT_V2PF 4  // 16-byte rows in flight in vert_glob2 (4 and 6 measured equal; 4: 108 VGPRs)
+#endif
+constexpr bool kVert2 = SIFT_VERT2 != 0;
+#ifndef SIFT_VGEN2
+#define SIFT_VGEN2 1  // ... and for the generic radii up to 32 (vert_glob_gen2)
+#endif
+constexpr bool kVertGen2 = SIFT_VGEN2 != 0;
 constexpr int kUR1 = SIFT_UR1;       // ... octaves >= 1 (SGPR budget: taps are SGPR operands)
 constexpr int kCG = kGX / 4;         // column groups of 4 outputs (16)
 constexpr int kRS = 64 / kCG;        // row sub-groups per wave (4)
@@ -78,6 +89,8 @@ constexpr int kPFH = 3;              // 16-byte reads in flight, horizontal pass
 
 __host__ __device__ constexpr int fl2(int a) { return a >> 1; }   // floor(a / 2)
 __host__ __device__ constexpr int cl2(int a) { return (a + 1) >> 1; }  // ceil(a / 2), a >= 0
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct GTile {
   int h, w, x0, y0;
@@ -207,6 +220,98 @@ __device__ __forceinline__ void vert_glob(const GTile& T, const cdouble* wp, dou
         if (lr + t < 8) Vw[(lr + t) * T.sw + kGX + col] = acc[t];
     }
   }
+}
+
+// The same vertical pass with two adjacent strip columns per lane and one
+// 16-byte load per row: the (64 + 2R) columns in ONE packed pass (no separate
+// halo pass) and half the load instructions of vert_glob -- the octave-1
+// launch is bound by its vertical loads' address processing (TA busy 0.84).
+// Column clamping: the pair (x, x+1) is read at xa = clamp(x, 0, w - 2); at
+// the left edge both columns are B[0] (the pair's first), at the right edge
+// both are B[w-1] (its second).  Same fma chain per column, bit-identical.
+template <int R>
+__device__ __forceinline__ void vert_glob2(const GTile& T, const cdouble* wp, double* V) {
+  constexpr int NC = kGX + 2 * R;  // even
+  constexpr int NPAIR = NC / 2;
+  static_assert(NPAIR <= 64, "one lane per column pair");
+  constexpr int NJ = 2 * R + 8;
+  constexpr int PF = NJ < SIFT_V2PF ? NJ : SIFT_V2PF;  // 16-byte rows in flight
+  const int p = T.lane;
+  if (p >= NPAIR) return;
+  const int yb = __builtin_amdgcn_readfirstlane(T.y0 + 8 * T.wv - R);
+  const int w8 = T.w * 8;
+  const int x = T.x0 - R + 2 * p;
+  const int xoff = clampi(x, 0, T.w - 2) * 8;
+  const bool lo_edge = x < 0, hi_edge = x >= T.w - 1;
+  int yy = yb;
+  auto ld = [&]() -> double2 {
+    const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(T.rsrc, xoff, clampi(yy, 0, T.h - 1) * w8, 0);
+    asm volatile("" : "+s"(yy));
+    yy += 1;
+    const double2 d = __builtin_bit_cast(double2, q);
+    return make_double2(hi_edge ? d.y : d.x, lo_edge ? d.x : d.y);
+  };
+  double a0[8], a1[8];
+  double2 v[NJ];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
+#pragma unroll
+  for (int j = 0; j < PF; ++j) v[j] = ld();
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (j + PF < NJ) v[j + PF] = ld();
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int k = j - t;
+      if (k >= 0 && k <= 2 * R) {
+        a0[t] = fma((double)wp[k], v[j].x, a0[t]);
+        a1[t] = fma((double)wp[k], v[j].y, a1[t]);
+      }
+    }
+    pin(a0);
+    pin(a1);
+  }
+  double* Vw = V + 8 * T.wv * T.sw + 2 * p;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) *reinterpret_cast<double2*>(Vw + t * T.sw) = make_double2(a0[t], a1[t]);
+}
+
+// vert_glob_gen with two columns per lane and 16-byte loads (radii up to 32:
+// the 64 + 2r columns in one packed pass); the same 8-row chunks over
+// zero-padded taps, so the same fma chains as vert_glob_gen.
+__device__ __forceinline__ void vert_glob_gen2(const GTile& T, int r, const cdouble* wp, double* V) {
+  const int NC = kGX + 2 * r, NJ = 2 * r + 8;
+  const int p = T.lane;
+  if (p >= NC / 2) return;
+  const int yb = T.y0 + 8 * T.wv - r;
+  const int x = T.x0 - r + 2 * p;
+  const int xoff = clampi(x, 0, T.w - 2) * 8;
+  const bool lo_edge = x < 0, hi_edge = x >= T.w - 1;
+  double a0[8], a1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
+  for (int jb = 0; jb < NJ; jb += 8) {
+    double2 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
+          T.rsrc, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, T.h - 1) * T.w * 8), 0);
+      const double2 d = __builtin_bit_cast(double2, q);
+      v[k] = make_double2(hi_edge ? d.y : d.x, lo_edge ? d.x : d.y);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        a0[t] = fma((double)wp[jb + k - t], v[k].x, a0[t]);  // zero-padded taps
+        a1[t] = fma((double)wp[jb + k - t], v[k].y, a1[t]);
+      }
+    pin(a0);
+    pin(a1);
+  }
+  double* Vw = V + 8 * T.wv * T.sw + 2 * p;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) *reinterpret_cast<double2*>(Vw + t * T.sw) = make_double2(a0[t], a1[t]);
 }
 
 __device__ __forceinline__ void vert_glob_gen(const GTile& T, int r, const cdouble* wp, double* V) {
@@ -468,7 +573,12 @@ __device__ __forceinline__ void vert_any_(std::integer_sequence<int, Rs...>, con
   if constexpr (OCT0) {
     ((!done && r == Rs ? (vert_o0<Rs>(T, wp, V), done = true) : false), ...);
   } else {
-    ((!done && r == Rs ? (vert_glob<Rs>(T, wp, V), done = true) : false), ...);
+    if (kVert2 && T.w >= 2) {
+      ((!done && r == Rs ? (vert_glob2<Rs>(T, wp, V), done = true) : false), ...);
+      if (kVertGen2 && !done && r <= 32) vert_glob_gen2(T, r, wp, V), done = true;
+    } else {
+      ((!done && r == Rs ? (vert_glob<Rs>(T, wp, V), done = true) : false), ...);
+    }
     if (!done) vert_glob_gen(T, r, wp, V);
   }
 }
@@ -501,8 +611,6 @@ __device__ __forceinline__ void store4(float* p, const double (&v)[4], int nvali
   for (int q = 0; q < 4; ++q)
     if (q < nvalid) p[q] = (float)v[q];
 }
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // 16-byte buffer store; lanes whose offset is past the plane are dropped by
 // the descriptor's range check.
