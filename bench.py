@@ -11,15 +11,16 @@ keypoint lists are all-gathered over RCCL (xGMI) each step: weak scaling.
 Prints ONE JSON line (rank 0).  Workload defaults to BASELINE.json's metric
 configuration: 3840x2160 (4K), 4 octaves x 5 scales.
 
-Roofline of the dominant kernel -- octave 0's k_gauss_dog launch, HBM-bound
-on its plane stores: algorithmic bytes per launch 4WH + 4 P_0 (S+3) +
-4 P_0 (S+2) (the input read, octave 0's Gaussian and DoG planes written in
-fp32; SURVEY.md §8d per octave), divided by that launch's HIP-event time on
-the context's stream (sift_timings.gauss_oct0_ms).  `traffic` is that
-kernel's HBM bytes per launch from the committed rocprofv3 PMC summary
-(profiles/*pmc*.json, tools/pmc_traffic.py) when it matches the config.
-`stage` reports the whole Gaussian+DoG pass (all octaves, one launch each)
-the same way: B_alg = 4WH + sum_o 4 P_o (S+3) + sum_o 4 P_o (S+2).
+`roofline` is SURVEY.md §8d's north-star quantity, the whole Gaussian+DoG
+pass (one k_gauss_dog launch per octave): B_alg = 4WH + sum_o 4 P_o (S+3) +
+sum_o 4 P_o (S+2) (the input read, every Gaussian and DoG plane written in
+fp32) divided by the pass's HIP-event time on the context's stream, one image
+at a time; `per_octave`, `pipelined`, `octave0` and `extrema_stage` break it
+down.  `traffic` is the pass's HBM bytes from the committed rocprofv3 PMC
+summary (profiles/*pmc*.json, tools/pmc_launches.py) when it matches the
+config.  `sustained` re-runs the pipelined loop for --sustain-s seconds after
+the timed region (a steady-state rate over thousands of images, beside the
+K-step `value`).
 """
 import argparse
 import glob
@@ -191,6 +192,9 @@ def main():
                          "detect_sharded_device: band octaves, all-gathered next-octave base, tail octaves one per "
                          "rank, block-major merge); strong scaling.  Defaults to 7680x4320, 6 octaves x 5 scales "
                          "unless --width/--height/--octaves are given")
+    ap.add_argument("--sustain-s", type=float, default=5.0,
+                    help="seconds of the same pipelined loop after the timed region, reported as `sustained` "
+                         "(0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
     ap.add_argument("--cpu-sample-js", default="1920x1080",
@@ -323,6 +327,35 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    # Steady state: the same pipelined loop for a few seconds (thousands of
+    # images; no per-image host work beyond the settle), its own clock.
+    sustained = None
+    if args.sustain_s > 0:
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ns, t1 = 0, time.perf_counter()
+        while True:
+            launch(NI + ns)
+            if ns >= nin - 1:
+                finish(NI + ns - (nin - 1), False)
+            ns += 1
+            if ns >= nin and time.perf_counter() - t1 >= args.sustain_s:
+                break
+        flush()
+        for i in range(max(0, ns - (nin - 1)), ns):
+            finish(NI + i, False)
+        for c in ctxs:
+            c.synchronize()
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter() - t1
+        if dist is not None:
+            e = torch.tensor([ts], dtype=torch.float64, device="cuda:%d" % dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            ts = float(e.item())
+        sustained = {"images_per_gpu": ns, "seconds": round(ts, 3),
+                     "value": round(world * ns * W * H / ts / 1e6, 3), "unit": "Mpix/s",
+                     "ms_per_image": round(ts / ns * 1e3, 4)}
     # After the timed region: the same detection alone (one image in flight,
     # nothing overlapping), so the kernel's isolated duration is on record
     # beside its pipelined one.
@@ -384,6 +417,7 @@ def main():
                                 if world > 1 else "single GPU"),
                 "planes": "fp32 out, fp64 accumulation/seeds",
             },
+            "sustained": sustained,
             "stages_ms": {k: round(v / NI, 4) for k, v in stage.items()},
             "keypoints": counts["keypoints"],
             "candidates": counts["candidates"],

@@ -194,7 +194,16 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
 
 template <bool LOWL>
 __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, const ExtremaLaunch L) {
-  const int u = L.u_begin + (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // Blocks are dealt round-robin over the 8 XCDs (separate L2s).  With
+  // xcd_band, XCD k scans the k-th contiguous range of units, so the lines
+  // shared by horizontally adjacent words (their halo columns) and by
+  // vertically adjacent strips (their halo rows) are fetched into one L2.
+  int lb = (int)blockIdx.x;
+  if (L.xcd_band) {
+    const int nb = (int)gridDim.x, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    lb = xc * q + min(xc, rm) + (lb >> 3);
+  }
+  const int u = L.u_begin + lb * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (u >= L.u_end) return;
   int o = 0;
   while (o + 1 < L.n_oct && u >= L.unit_off[o + 1]) ++o;
@@ -341,6 +350,9 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
     const long v = e ? std::strtol(e, nullptr, 10) : 0;
     return (v > 0 && v <= 160 * 1024) ? (int)v : 0;
   }();
+  // SIFT_XXCD=0: plain round-robin block order (experiments)
+  static const int xxcd = [] { const char* e = std::getenv("SIFT_XXCD"); return e ? std::atoi(e) : 1; }();
+  L.xcd_band = xxcd != 0;
   const void* fn = L.lowbitmap ? (const void*)k_extrema<true> : (const void*)k_extrema<false>;
   if (xlds > 65536) {
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, xlds);

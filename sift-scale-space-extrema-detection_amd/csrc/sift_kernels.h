@@ -67,6 +67,7 @@ struct ExtremaLaunch {
   int u_begin, u_end;            // units of this launch (a range of octaves)
   int exact_planes;              // DoG planes are the data itself (caller-supplied): no fp32 ties
   int ng;                        // scale groups per (strip, word)
+  int xcd_band;                  // 1: block -> units so that each XCD scans a contiguous range of units
   float c_lo, c_hi;              // |v| < c_lo: certainly low contrast; |v| >= c_hi: certainly not
   int unit_off[kMaxOctaves + 1]; // first unit of each octave
   int nw[kMaxOctaves];           // words per row
