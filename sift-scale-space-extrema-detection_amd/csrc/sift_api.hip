@@ -53,6 +53,7 @@ enum DogSource { kNone = 0, kNative = 1, kForeign = 2 };
 // the kept keypoints per (octave, scale) block from kBlk on.
 constexpr int kBlk = 64;
 constexpr int kCntAll = kBlk + kBlkWords;  // per-block counts, block starts, order flag (sift_kernels.h)
+constexpr int kMaxBands = 16;              // row bands per octave of a banded Gaussian pass
 
 }  // namespace
 
@@ -123,6 +124,12 @@ struct sift_ctx {
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
   hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
+  // Banded pass (octave_bands): octave o >= 1 runs on ost[o], band j of octave
+  // o signals ev_band[o][j]; ev_bfork starts the band streams after the setup.
+  hipStream_t ost[kMaxOctaves]{};
+  hipEvent_t ev_band[kMaxOctaves][kMaxBands]{};
+  hipEvent_t ev_bfork = nullptr;
+  int bands_used = 0;              // bands per octave of the last build (1 = one launch per octave)
   sift_timings tm{};
   std::vector<double> oct_ms;      // per-octave Gaussian+DoG launch time of the last build
 };
@@ -273,6 +280,12 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   for (auto& e : ctx->ev_go)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_heavy) (void)hipEventDestroy(ctx->ev_heavy);
+  for (auto& st : ctx->ost)
+    if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
+  for (auto& row : ctx->ev_band)
+    for (auto& e : row)
+      if (e) (void)hipEventDestroy(e);
+  if (ctx->ev_bfork) (void)hipEventDestroy(ctx->ev_bfork);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
   for (auto& e : ctx->ev_oct)
     if (e) (void)hipEventDestroy(e);
@@ -408,6 +421,42 @@ static bool fuse_enabled(const sift_params* p) {
   return env || (p->flags & SIFT_F_FUSED_EXTREMA);
 }
 
+// Banded Gaussian pass.  Octave 0 is bound by its HBM stores, the small
+// octaves by fp64 issue and load addressing; one launch per octave runs them
+// one after the other.  With bands, octave 0 is launched as SIFT_OBANDS row
+// bands on the context stream and every following octave (up to the first
+// split-pass octave) as bands on a stream of its own, each band waiting only
+// for the bands of the previous octave its seed rows come from (its rows
+// plus the vertical radius), so the small octaves run beside octave 0's
+// stores instead of after them.  The planes are the same bit for bit (every
+// tile runs the same code; only the launch a tile belongs to changes).
+static int octave_bands() {
+  static const int nb = [] {
+    const char* e = std::getenv("SIFT_OBANDS");
+    const int v = e ? std::atoi(e) : 1;
+    return std::max(1, std::min(v, kMaxBands));
+  }();
+  return nb;
+}
+
+static int ensure_band_streams(sift_ctx* ctx, int n_oct) {
+  if (!ctx->ev_bfork) HIPCHK(hipEventCreateWithFlags(&ctx->ev_bfork, hipEventDisableTiming));
+  for (int o = 0; o < n_oct; ++o) {
+    if (o >= 1 && !ctx->ost[o]) HIPCHK(hipStreamCreateWithFlags(&ctx->ost[o], hipStreamNonBlocking));
+    for (auto& e : ctx->ev_band[o])
+      if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  return SIFT_OK;
+}
+
+// Band j of nb over t tile rows: [j t / nb, (j + 1) t / nb).
+static int band_begin(int j, int t, int nb) { return (int)((long long)j * t / nb); }
+static int band_of(int row, int t, int nb) {
+  int j = 0;
+  while (j + 1 < nb && band_begin(j + 1, t, nb) <= row) ++j;
+  return j;
+}
+
 // overlap_extrema: launch each octave's extrema scan on the side stream as
 // soon as its DoG planes exist, overlapping the next octaves' Gaussian
 // kernels (memory-bound scans beside FMA-bound small octaves).
@@ -502,6 +551,20 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     ctx->xseed_w = (P.oct[P.O - 1].w + 1) / 2;
     HIPCHK(ctx->xseed.ensure((size_t)ctx->xseed_h * ctx->xseed_w * sizeof(double)));
   }
+  // Banded pass: octaves o_first .. ob-1 in row bands (octave_bands above).
+  int nbands = octave_bands(), ob = o_first;
+  if (nbands > 1 && o_first == 0 && !nf && !overlap && !ctx->hi) {
+    while (ob < P.O && !gauss_vsplit(P, ob)) ++ob;
+    if (ob - o_first < 2) ob = o_first;
+  }
+  if (ob == o_first) nbands = 1;
+  ctx->bands_used = nbands;
+  if (nbands > 1) {
+    rc = ensure_band_streams(ctx, ob);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(ctx->ev_bfork, ctx->stream));
+    for (int o = o_first + 1; o < ob; ++o) HIPCHK(hipStreamWaitEvent(ctx->ost[o], ctx->ev_bfork, 0));
+  }
   for (int o = o_first; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
     GaussLaunch L{};
@@ -532,10 +595,34 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     }
     L.l64 = P.oct[o].l64_off >= 0 ? ctx->l64.as<double>() + P.oct[o].l64_off : nullptr;
     L.vsplit = gauss_vsplit(P, o) ? ctx->vsplit.as<double>() : nullptr;
-    HIPCHK(launch_gauss_dog(P, L, ls));
+    if (nbands > 1) {
+      // octaves past the banded ones follow the last banded octave on its stream
+      if (o > o_first) ls = ctx->ost[std::min(o, ob - 1)];
+      if (o < ob) {
+        const int t = gauss_tile_rows(P, o);
+        int waited = -1;
+        for (int j = 0; j < nbands; ++j) {
+          const int t0 = band_begin(j, t, nbands), t1 = band_begin(j + 1, t, nbands);
+          if (o > o_first) {  // the previous octave's bands holding this band's seed rows
+            const int ylast = std::min(oc.h, kGaussTileRows * t1) - 1;
+            const int qmax = std::min(oc.h - 1, ylast + oc.rmax + 8);
+            const int tp = gauss_tile_rows(P, o - 1);
+            const int need = band_of(std::min(tp - 1, 2 * qmax / kGaussTileRows), tp, nbands);
+            for (int b = waited + 1; b <= need; ++b) HIPCHK(hipStreamWaitEvent(ls, ctx->ev_band[o - 1][b], 0));
+            waited = std::max(waited, need);
+          }
+          if (t1 > t0) HIPCHK(launch_gauss_dog(P, L, ls, t0, t1));
+          HIPCHK(hipEventRecord(ctx->ev_band[o][j], ls));
+        }
+      } else {
+        HIPCHK(launch_gauss_dog(P, L, ls));
+      }
+    } else {
+      HIPCHK(launch_gauss_dog(P, L, ls));
+    }
     if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ls));
     HIPCHK(hipEventRecord(ctx->ev_go[o], ls));
-    if (ls != ctx->stream) {
+    if (ls != ctx->stream && ls == ctx->hi) {
       HIPCHK(hipEventRecord(ctx->ev_hi_join, ls));
       HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_hi_join, 0));
     }
@@ -545,6 +632,10 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
       rc = extrema_scan(ctx, o, o + 1, ctx->side);
       if (rc) return rc;
     }
+  }
+  if (nbands > 1) {  // the band streams join the context stream
+    for (int o = o_first + 1; o < ob; ++o) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_go[o], 0));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_go[P.O - 1], 0));
   }
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   if (overlap) {

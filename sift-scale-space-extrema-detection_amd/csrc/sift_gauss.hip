@@ -67,6 +67,12 @@ constexpr int kUR = 16;              // radii with unrolled code (octave 0)
 #ifndef SIFT_MINW1
 #define SIFT_MINW1 1
 #endif
+#ifndef SIFT_W96
+#define SIFT_W96 1  // 96-column kernel: minimum waves per SIMD (register budget; experiments)
+#endif
+#ifndef SIFT_PF96
+#define SIFT_PF96 2
+#endif
 #ifndef SIFT_VERT2
 #define SIFT_VERT2 1  // octaves >= 1: two columns per lane, 16-byte loads (vert_glob2)
 #endif
@@ -96,7 +102,8 @@ struct GTile {
   int h, w, x0, y0;
   int bx;              // tile column
   int lane, wv;        // wv wave-uniform (SGPR)
-  int cg, rs;          // horizontal mapping
+  int cg, rs;          // horizontal mapping (64-column tiles)
+  int icg[3], irow[3]; // 96-column tiles: item i of the lane = columns 4 icg .. +3 of wave row irow
   int sw;              // strip stride
   int hrm;             // octave 0: ceil(RM / 2) of the staged region
   const double* S0;    // octave 0: staged input region [..][kBW0]
@@ -229,9 +236,9 @@ __device__ __forceinline__ void vert_glob(const GTile& T, const cdouble* wp, dou
 // Column clamping: the pair (x, x+1) is read at xa = clamp(x, 0, w - 2); at
 // the left edge both columns are B[0] (the pair's first), at the right edge
 // both are B[w-1] (its second).  Same fma chain per column, bit-identical.
-template <int R>
+template <int R, int TW = kGX>
 __device__ __forceinline__ void vert_glob2(const GTile& T, const cdouble* wp, double* V) {
-  constexpr int NC = kGX + 2 * R;  // even
+  constexpr int NC = TW + 2 * R;  // even
   constexpr int NPAIR = NC / 2;
   static_assert(NPAIR <= 64, "one lane per column pair");
   constexpr int NJ = 2 * R + 8;
@@ -242,34 +249,45 @@ __device__ __forceinline__ void vert_glob2(const GTile& T, const cdouble* wp, do
   const int w8 = T.w * 8;
   const int x = T.x0 - R + 2 * p;
   const int xoff = clampi(x, 0, T.w - 2) * 8;
-  const bool lo_edge = x < 0, hi_edge = x >= T.w - 1;
+  double a0[8], a1[8];
+  double2 v[NJ];
+  auto run = [&](auto ld) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) v[j] = ld();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (j + PF < NJ) v[j + PF] = ld();
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int k = j - t;
+        if (k >= 0 && k <= 2 * R) {
+          a0[t] = fma((double)wp[k], v[j].x, a0[t]);
+          a1[t] = fma((double)wp[k], v[j].y, a1[t]);
+        }
+      }
+      pin(a0);
+      pin(a1);
+    }
+  };
   int yy = yb;
-  auto ld = [&]() -> double2 {
+  auto raw = [&]() -> double2 {
     const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(T.rsrc, xoff, clampi(yy, 0, T.h - 1) * w8, 0);
     asm volatile("" : "+s"(yy));
     yy += 1;
-    const double2 d = __builtin_bit_cast(double2, q);
-    return make_double2(hi_edge ? d.y : d.x, lo_edge ? d.x : d.y);
+    return __builtin_bit_cast(double2, q);
   };
-  double a0[8], a1[8];
-  double2 v[NJ];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
-#pragma unroll
-  for (int j = 0; j < PF; ++j) v[j] = ld();
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    if (j + PF < NJ) v[j + PF] = ld();
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int k = j - t;
-      if (k >= 0 && k <= 2 * R) {
-        a0[t] = fma((double)wp[k], v[j].x, a0[t]);
-        a1[t] = fma((double)wp[k], v[j].y, a1[t]);
-      }
-    }
-    pin(a0);
-    pin(a1);
+  // Tiles whose strip columns x0 - R .. x0 + TW + R - 1 all lie inside the
+  // plane (wave-uniform) need no edge selects (4 VALU per 16-byte row).
+  if (T.x0 - R >= 0 && T.x0 + TW + R <= T.w) {
+    run(raw);
+  } else {
+    const bool lo_edge = x < 0, hi_edge = x >= T.w - 1;
+    run([&]() -> double2 {
+      const double2 d = raw();
+      return make_double2(hi_edge ? d.y : d.x, lo_edge ? d.x : d.y);
+    });
   }
   double* Vw = V + 8 * T.wv * T.sw + 2 * p;
 #pragma unroll
@@ -489,6 +507,48 @@ __device__ __forceinline__ void horz_full(const GTile& T, const cdouble* wp, con
   }
 }
 
+// 96-column tiles (octaves >= 1 whose radii are all unrolled): 24 column
+// groups x 8 rows = 192 items of 4 columns x 1 row, three per lane (item i =
+// lane + 64 i), so the 64 + 2r-column vertical pass of a 64-wide tile becomes
+// a 96 + 2r one with (96 + 2r) / 128 instead of (64 + 2r) / 128 of its lanes
+// busy and a third fewer loads per output.  Same fma chain per output.
+template <int R>
+__device__ __forceinline__ void horz_full96(const GTile& T, const cdouble* wp, const double* V, double (&out)[3][4]) {
+  constexpr int NP = R + 2;  // double2 pairs per row
+  constexpr int PF96 = SIFT_PF96;  // 16-byte reads in flight per item
+  const double* rp[3];
+  double2 u[3][NP];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    rp[i] = V + (8 * T.wv + T.irow[i]) * T.sw + 4 * T.icg[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[i][q] = 0.0;
+  }
+#pragma unroll
+  for (int n2 = 0; n2 < PF96 && n2 < NP; ++n2)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i][n2] = *reinterpret_cast<const double2*>(rp[i] + 2 * n2);
+#pragma unroll
+  for (int n2 = 0; n2 < NP; ++n2) {
+    if (n2 + PF96 < NP)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) u[i][n2 + PF96] = *reinterpret_cast<const double2*>(rp[i] + 2 * (n2 + PF96));
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * n2 + e;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = n - q;
+        if (k >= 0 && k <= 2 * R)
+#pragma unroll
+          for (int i = 0; i < 3; ++i) out[i][q] = fma((double)wp[k], e ? u[i][n2].y : u[i][n2].x, out[i][q]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pin(out[i]);
+  }
+}
+
 __device__ __forceinline__ void horz_full_gen(const GTile& T, int r, const cdouble* wp, const double* V,
                                               double (&out)[kNR][4]) {
   const int NV = 2 * r + 4;
@@ -593,6 +653,19 @@ __device__ __forceinline__ void horz_any_(std::integer_sequence<int, Rs...>, con
     ((!done && r == Rs ? (horz_full<Rs>(T, wp, V, out), done = true) : false), ...);
     if (!done) horz_full_gen(T, r, wp, V, out);
   }
+}
+
+template <int... Rs>
+__device__ __forceinline__ void vert96_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
+                                           const cdouble* wp, double* V) {
+  bool done = false;
+  ((!done && r == Rs ? (vert_glob2<Rs, 96>(T, wp, V), done = true) : false), ...);
+}
+template <int... Rs>
+__device__ __forceinline__ void horz96_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
+                                           const cdouble* wp, const double* V, double (&out)[3][4]) {
+  bool done = false;
+  ((!done && r == Rs ? (horz_full96<Rs>(T, wp, V, out), done = true) : false), ...);
 }
 
 // Unrolled radii 0..RMAX.
@@ -700,8 +773,13 @@ __device__ __forceinline__ void fused_decide(const Pyramid& P, const GaussLaunch
 
 // SWC > 0: compile-time strip stride (immediate LDS offsets); 0: L.sw.
 // RMAX: radii with unrolled code.  XF: extrema decisions fused (above).
-template <bool OCT0, int SWC, int RMAX, bool XF>
-__global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
+// TW: tile width (64; 96 for octaves >= 1 whose radii are all unrolled,
+// horz_full96); NI items of 4 columns x 1 row per lane in the horizontal pass
+// and the epilogue.
+template <bool OCT0, int SWC, int RMAX, bool XF, int TW = kGX>
+__global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1)) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
+  static_assert(TW == kGX || (TW == 96 && !OCT0 && !XF && RMAX <= 16), "96-column tiles: octaves >= 1, unrolled radii");
+  constexpr int NI = TW == kGX ? kNR : 3;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const Octave& oc = P.oct[L.o];
   // 1D grid: block -> (scale group, tile).  Blocks are dispatched round-robin
@@ -714,17 +792,28 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     lb = xc * q + min(xc, rm) + (lb >> 3);
   }
   const int bz = lb % L.G, bt = lb / L.G;
-  const int bx = bt % L.gx, by = bt / L.gx;
+  const int bx = bt % L.gx, by = bt / L.gx + L.by0;
   GTile T;
   T.bx = bx;
   T.h = oc.h;
   T.w = oc.w;
-  T.x0 = bx * (XF ? kFX : kGX);
+  T.x0 = bx * (XF ? kFX : TW);
   T.y0 = by * (XF ? kFY : kGY);
   T.lane = threadIdx.x & 63;
   T.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   T.cg = T.lane & (kCG - 1);
   T.rs = T.lane / kCG;
+  if constexpr (TW == 96) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int idx = T.lane + 64 * i;
+      T.icg[i] = idx % 24;
+      T.irow[i] = idx / 24;
+    }
+  }
+  // item i of the lane: wave row irw(i), first column x0 + 4 icg(i)
+  auto irw = [&](int i) { return TW == kGX ? T.rs + kRS * i : T.irow[i]; };
+  auto icg = [&](int i) { return TW == kGX ? T.cg : T.icg[i]; };
   T.sw = SWC > 0 ? SWC : L.sw;
   T.hrm = cl2(oc.rmax);
   if (!OCT0)
@@ -758,20 +847,19 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     }
   }
   const long long plane = (long long)T.h * T.w;
-  const int x = T.x0 + 4 * T.cg;
-  const int nvalid = T.w - x;
   // Pixels this block stores: all of its tile, or with fused extrema the
   // kFX x kFY it owns (the last tile of a row / column: all it computes).
-  const bool own_c = !XF || 4 * T.cg < kFX || bx == L.gx - 1;
-  bool own[kNR];
-  // Per-lane byte offsets of its two output rows in a plane (past the plane
-  // or not owned: the store is dropped).
-  int voff[kNR];
+  bool own[NI];
+  // Per-lane byte offsets of its output items in a plane (past the plane or
+  // not owned: the store is dropped).
+  int voff[NI];
 #pragma unroll
-  for (int i = 0; i < kNR; ++i) {
-    const int r = 8 * T.wv + T.rs + kRS * i;
+  for (int i = 0; i < NI; ++i) {
+    const int r = 8 * T.wv + irw(i);
     const int y = T.y0 + r;
-    own[i] = y < T.h && nvalid > 0 && own_c && (!XF || r < kFY || by == L.gy - 1);
+    const int x = T.x0 + 4 * icg(i);
+    const bool own_c = !XF || 4 * icg(i) < kFX || bx == L.gx - 1;
+    own[i] = y < T.h && T.w - x > 0 && own_c && (!XF || r < kFY || by == L.gy - 1);
     voff[i] = own[i] ? (y * T.w + x) * 4 : 0x7ffffff0;
   }
 
@@ -783,7 +871,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
   __syncthreads();  // staged region / zeroed strip visible to every wave
 
   const bool st = !(L.dbg & 1);  // dbg 1: timing without plane stores
-  double lprev[kNR][4];
+  double lprev[NI][4];
   for (int s = s_first; s < s_end; ++s) {
     const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
     // Per-lane indices made opaque each scale: otherwise the compiler hoists
@@ -791,20 +879,30 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     // keeps it all live (dozens of VGPRs, half the occupancy).
     GTile Ts = T;
     asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
-    if constexpr (!OCT0) {
-      if (L.vsplit) vert_copy(Ts, oc.rad[s], L.vsplit + (long long)s * plane, V);
-      else vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
-    } else {
-      vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
+    if constexpr (TW == 96) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Ts.icg[i]), "+v"(Ts.irow[i]));
     }
-    wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
-    double out[kNR][4];
-    horz_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V, out);
+    double out[NI][4];
+    if constexpr (TW == 96) {
+      vert96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V);
+      wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
+      horz96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V, out);
+    } else {
+      if constexpr (!OCT0) {
+        if (L.vsplit) vert_copy(Ts, oc.rad[s], L.vsplit + (long long)s * plane, V);
+        else vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
+      } else {
+        vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
+      }
+      wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
+      horz_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V, out);
+    }
     wave_lds_fence();  // strip rows read before the next scale overwrites them
 
-    double d[kNR][4];
+    double d[NI][4];
 #pragma unroll
-    for (int i = 0; i < kNR; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
     if (s >= s_begin && (st || out[0][0] == 12345.0)) {
@@ -813,17 +911,18 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
         if (L.gauss) {
           const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L.gauss + s * plane, 0, pb, 0x00020000);
 #pragma unroll
-          for (int i = 0; i < kNR; ++i) bstore4(rg, voff[i], out[i]);
+          for (int i = 0; i < NI; ++i) bstore4(rg, voff[i], out[i]);
         }
         if (s > 0) {
           const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L.dog + (s - 1) * plane, 0, pb, 0x00020000);
 #pragma unroll
-          for (int i = 0; i < kNR; ++i) bstore4(rd, voff[i], d[i]);
+          for (int i = 0; i < NI; ++i) bstore4(rd, voff[i], d[i]);
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < kNR; ++i) {
-          const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
+        for (int i = 0; i < NI; ++i) {
+          const int y = T.y0 + 8 * T.wv + irw(i);
+          const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
           if (own[i]) {
             const long long pp = (long long)y * T.w + x;
             if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
@@ -852,8 +951,9 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     if (L.l64 && s >= s_begin) {  // fp64 plane for the exact passes
       double* lp = L.l64 + s * plane;
 #pragma unroll
-      for (int i = 0; i < kNR; ++i) {
-        const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
+      for (int i = 0; i < NI; ++i) {
+        const int y = T.y0 + 8 * T.wv + irw(i);
+        const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
         if (own[i]) {
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -863,8 +963,9 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
     }
     if (s == P.S && L.next_seed && s >= s_begin) {
 #pragma unroll
-      for (int i = 0; i < kNR; ++i) {
-        const int y = T.y0 + 8 * T.wv + T.rs + kRS * i;
+      for (int i = 0; i < NI; ++i) {
+        const int y = T.y0 + 8 * T.wv + irw(i);
+        const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
         if (own[i] && !(y & 1)) {
           double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
           sd[0] = out[i][0];
@@ -873,7 +974,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : SIFT_MINW1) void k_gauss_dog(const 
       }
     }
 #pragma unroll
-    for (int i = 0; i < kNR; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
   }
@@ -923,6 +1024,14 @@ bool gauss_vsplit(const Pyramid& P, int o) {
 
 static bool staged0(const Pyramid& P, int o) { return o == 0 && !gauss_needs_base0(P); }
 
+// 96-column tiles (horz_full96) for octaves >= 1 whose radii all have
+// unrolled code and no split pass (SIFT_TW96=0: always 64, experiments).
+static int tile_w(const Pyramid& P, int o) {
+  static const int tw96 = [] { const char* e = std::getenv("SIFT_TW96"); return e ? std::atoi(e) : 1; }();
+  const Octave& oc = P.oct[o];
+  return (tw96 && o >= 1 && kVert2 && oc.rmax <= kUR1 && oc.w >= 2 && !gauss_vsplit(P, o)) ? 96 : kGX;
+}
+
 constexpr int kSW0 = 2 * (kCG - 1) + 8 + 6;   // octave-0 strip stride for rmax <= 8
 constexpr int kSW1 = 2 * (kCG - 1) + kUR + 6;  // ... rmax <= kUR
 
@@ -933,7 +1042,8 @@ constexpr int kSW1 = 2 * (kCG - 1) + kUR + 6;  // ... rmax <= kUR
 static int strip_stride(const Pyramid& P, int o) {
   const int R = P.oct[o].rmax;
   if (staged0(P, o)) return R <= 8 ? kSW0 : kSW1;
-  int sw = R <= kUR1 ? kGX + 2 * R + 4 : kGX + 2 * R + 12;
+  const int tw = tile_w(P, o);
+  int sw = R <= kUR1 ? tw + 2 * R + 4 : tw + 2 * R + 12;
   if (sw % 4 == 0) sw += 2;
   return sw;
 }
@@ -1014,7 +1124,8 @@ static int scale_groups(const Pyramid& P, int o) {
   // has ~1.5 blocks per CU -- 60x68 tiles: 1 group; 30x34: 1 (G=2: 116 us,
   // G=4: 126-140 us, G=1: 103 us); 15x17: 2 (70.8 us; G=1 94 us, G=4 85 us).
   const Octave& oc = P.oct[o];
-  const long long tiles = (long long)((oc.w + kGX - 1) / kGX) * ((oc.h + kGY - 1) / kGY);
+  const int tw = tile_w(P, o);
+  const long long tiles = (long long)((oc.w + tw - 1) / tw) * ((oc.h + kGY - 1) / kGY);
   int g = 1;
   while (g < P.NS && tiles * g < 400) ++g;
   return g;
@@ -1033,13 +1144,23 @@ hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st)
   return hipGetLastError();
 }
 
-hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
+int gauss_tile_rows(const Pyramid& P, int o) { return (P.oct[o].h + kGY - 1) / kGY; }
+
+hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin, int ty_end) {
+  static_assert(kGY == kGaussTileRows, "tile rows");
   const Octave& oc = P.oct[L.o];
   if (L.fuse && !gauss_can_fuse(P, L.o)) return hipErrorInvalidValue;
   const int G = scale_groups(P, L.o);
   split_scales(P, L.o, G, L.gb);
-  L.gx = L.fuse ? fused_words_per_row(oc.w) : (oc.w + kGX - 1) / kGX;
+  const int tw = tile_w(P, L.o);
+  L.gx = L.fuse ? fused_words_per_row(oc.w) : (oc.w + tw - 1) / tw;
   L.gy = L.fuse ? (oc.h - 2 + kFY - 1) / kFY : (oc.h + kGY - 1) / kGY;
+  L.by0 = 0;
+  if (ty_end >= 0) {  // a band of tile rows
+    if (L.fuse || L.vsplit || ty_begin < 0 || ty_end > L.gy || ty_begin >= ty_end) return hipErrorInvalidValue;
+    L.by0 = ty_begin;
+    L.gy = ty_end - ty_begin;
+  }
   L.G = L.fuse ? 1 : G;
   if (L.fuse && L.gx != L.X.nw) return hipErrorInvalidValue;
   // XCD-banded tile order for octaves >= 1 (SIFT_XCD_BAND: bit o-1 of the
@@ -1073,6 +1194,8 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st) {
   if (L.fuse) {  // staged octave 0 (gauss_can_fuse)
     if (L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, true>), grid, dim3(256), lds, st, P, L);
     else hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, true>), grid, dim3(256), lds, st, P, L);
+  } else if (tw == 96) {
+    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false, 96>), grid, dim3(256), lds, st, P, L);
   } else if (staged0(P, L.o) && L.sw == kSW0) {
     hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, false>), grid, dim3(256), lds, st, P, L);
   } else if (staged0(P, L.o)) {

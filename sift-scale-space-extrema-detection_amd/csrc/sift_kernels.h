@@ -50,6 +50,7 @@ struct GaussLaunch {
   int dbg;            // timing experiments (SIFT_GAUSS_DBG): bit 0 = no plane stores
   int gb[kMaxScales + 1];  // scale groups: group g computes scales gb[g] .. gb[g+1]-1
   int gx, gy, G;      // tiles per row, tile rows, scale groups (1D grid of gx gy G blocks)
+  int by0;            // first tile row of this launch (a band of tile rows by0 .. by0 + gy - 1)
   int xcd_band;       // 1: block -> tile so that each XCD runs a contiguous band of tile rows
 };
 
@@ -135,7 +136,11 @@ bool gauss_can_fuse(const Pyramid& P, int o);
 // of the input (4 H W doubles) instead of the staged input region.
 bool gauss_needs_base0(const Pyramid& P);
 hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st);
-hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st);
+// ty_end >= 0: only tile rows [ty_begin, ty_end) of the octave (a band;
+// not for fused or split-pass octaves).
+hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin = 0, int ty_end = -1);
+int gauss_tile_rows(const Pyramid& P, int o);  // tile rows of octave o's Gaussian launch
+constexpr int kGaussTileRows = 32;             // output rows per tile row
 // Tile columns of a fused launch over a w-column octave (= bitmap words per row).
 inline int fused_words_per_row(int w) { return w > 2 ? (w - 2 + kFX - 1) / kFX : 1; }
 hipError_t launch_dog_from_gauss(const float* g, float* d, long long plane, int nd, hipStream_t st);
