@@ -294,6 +294,47 @@ __device__ __forceinline__ void vert_glob2(const GTile& T, const cdouble* wp, do
   for (int t = 0; t < 8; ++t) *reinterpret_cast<double2*>(Vw + t * T.sw) = make_double2(a0[t], a1[t]);
 }
 
+// Generic radii: rows in chunks of 8 (chunk base jb), output t of the
+// wave's 8 rows takes tap jb + k - t of chunk row k.  Taps outside [0, 2r]
+// are zero and fma(0, v, acc) == acc, so the chunks skip them: the first
+// chunk (jb = 0) has no taps for k < t, a tail chunk none for k - t > M =
+// 2r - jb (and loads no row k > M + 7, past the window).  The same fma
+// chains as the zero-padded form, term for term.
+template <int M>
+struct VChunk {
+  static constexpr int kRows = M + 8 < 8 ? M + 8 : 8;  // rows k <= M + 7
+  template <bool FIRST, class Fma>
+  __device__ __forceinline__ static void run(Fma&& f) {
+#pragma unroll
+    for (int k = 0; k < kRows; ++k)
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (!(FIRST && k < t) && k - t <= M) f(k, t);
+  }
+};
+// m = 2r - jb (even).  Full chunks, and tail chunks with m >= 0, run all 64
+// (k, t) pairs (a tail's few taps past 2r are zero padding); the first chunk
+// skips its k < t triangle, the last chunks with m < 0 their rows past the
+// window -- five bodies, so the register allocation of the kernel is not
+// driven by a variant per radius.
+template <bool FIRST, class Body>
+__device__ __forceinline__ void vchunk_dispatch(int m, Body&& body) {
+  using F = std::integral_constant<bool, FIRST>;
+  using N = std::integral_constant<bool, false>;
+  if (FIRST) {
+    if (m >= 7) body(VChunk<7>{}, F{});
+    else body(VChunk<7>{}, N{});  // 2r < 7: zero-padded taps on both sides
+  } else if (m >= 0) {
+    body(VChunk<7>{}, N{});
+  } else if (m == -2) {
+    body(VChunk<-2>{}, N{});
+  } else if (m == -4) {
+    body(VChunk<-4>{}, N{});
+  } else {
+    body(VChunk<-6>{}, N{});
+  }
+}
+
 // vert_glob_gen with two columns per lane and 16-byte loads (radii up to 32:
 // the 64 + 2r columns in one packed pass); the same 8-row chunks over
 // zero-padded taps, so the same fma chains as vert_glob_gen.
@@ -308,25 +349,27 @@ __device__ __forceinline__ void vert_glob_gen2(const GTile& T, int r, const cdou
   double a0[8], a1[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
-  for (int jb = 0; jb < NJ; jb += 8) {
+  auto chunk = [&](int jb, auto C, auto first) {
+    using CC = decltype(C);
     double2 v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < CC::kRows; ++k) {
       const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
           T.rsrc, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, T.h - 1) * T.w * 8), 0);
       const double2 d = __builtin_bit_cast(double2, q);
       v[k] = make_double2(hi_edge ? d.y : d.x, lo_edge ? d.x : d.y);
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        a0[t] = fma((double)wp[jb + k - t], v[k].x, a0[t]);  // zero-padded taps
-        a1[t] = fma((double)wp[jb + k - t], v[k].y, a1[t]);
-      }
+    const cdouble* w = wp + jb;
+    CC::template run<decltype(first)::value>([&](int k, int t) {
+      a0[t] = fma((double)w[k - t], v[k].x, a0[t]);
+      a1[t] = fma((double)w[k - t], v[k].y, a1[t]);
+    });
     pin(a0);
     pin(a1);
-  }
+  };
+  vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
+  for (int jb = 8; jb < NJ; jb += 8)
+    vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
   double* Vw = V + 8 * T.wv * T.sw + 2 * p;
 #pragma unroll
   for (int t = 0; t < 8; ++t) *reinterpret_cast<double2*>(Vw + t * T.sw) = make_double2(a0[t], a1[t]);
@@ -387,17 +430,19 @@ __global__ __launch_bounds__(256) void k_gauss_vert(const Pyramid P, int o, cons
   double acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = 0.0;
-  for (int jb = 0; jb < NJ; jb += 8) {
+  auto chunk = [&](int jb, auto C, auto first) {
+    using CC = decltype(C);
     double v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < CC::kRows; ++k)
       v[k] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, h - 1) * w * 8));
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = fma((double)wp[jb + k - t], v[k], acc[t]);  // zero-padded taps
+    const cdouble* wq = wp + jb;
+    CC::template run<decltype(first)::value>([&](int k, int t) { acc[t] = fma((double)wq[k - t], v[k], acc[t]); });
     pin(acc);
-  }
+  };
+  vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
+  for (int jb = 8; jb < NJ; jb += 8)
+    vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
   if (x < w) {
     double* dst = vout + (long long)s * h * w + (long long)y0 * w + x;
 #pragma unroll
