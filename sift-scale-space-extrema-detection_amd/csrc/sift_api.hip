@@ -85,6 +85,7 @@ struct sift_ctx {
   int slot_cap = 0;         // slots the refinement runs over
   bool ext_pending = false; // extrema launched, counts not yet read back
   bool has_keep = false;    // slots carry keep flags
+  bool slots_rows = false;  // slots are the extrema stage's emission (row offsets in rowoff): band order applies
   bool scans_done = false;  // build_common already launched the extrema scans (side stream)
   bool counters_zeroed = false;  // extrema_prepare zeroed the refinement counters too
   bool detect_pending = false;   // sift_detect_device_async enqueued, sift_detect_wait not yet called
@@ -113,6 +114,7 @@ struct sift_ctx {
   DBuf lowbitmap, lowrowcount, lowrowoff;      // low-contrast list (SIFT_F_LOW_CONTRAST_LIST)
   DBuf low_key, low_val, late_key, late_val;
   DBuf keep, pos;                              // keypoint compaction
+  DBuf band_cnt, band_first, band_start, perm;  // refinement band order
   DBuf status, kp_tmp, kp, uncertain;          // refinement
   DBuf xseed, kp_key;                          // next-octave base, keypoint origins
   DBuf merge_tab;                              // sift_merge_keypoint_blocks_device tables
@@ -273,7 +275,8 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->xseed, &ctx->kp_key, &ctx->counters,
                   &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab,
                   &ctx->lowbitmap, &ctx->lowrowcount, &ctx->lowrowoff, &ctx->low_key, &ctx->low_val,
-                  &ctx->late_key, &ctx->late_val};
+                  &ctx->late_key, &ctx->late_val, &ctx->band_cnt, &ctx->band_first, &ctx->band_start,
+                  &ctx->perm};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -969,6 +972,7 @@ static int extrema_finish(sift_ctx* ctx) {
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->slot_cap = (int)ctx->cand_cap;
   ctx->has_keep = true;
+  ctx->slots_rows = true;
   ctx->ext_pending = true;
   return SIFT_OK;
 }
@@ -1062,6 +1066,41 @@ static int refine_enqueue(sift_ctx* ctx) {
     R.kp = ctx->kp_tmp.as<Keypoint>();
     R.uncertain = ctx->uncertain.as<unsigned>();
     R.counters = cnt;
+    R.perm = nullptr;
+    static const int band_order = [] { const char* e = std::getenv("SIFT_BAND_ORDER"); return e ? std::atoi(e) : 1; }();
+    if (band_order && ctx->slots_rows) {
+      BandOrder B{};
+      B.n_oct = P.O;
+      B.S = P.S;
+      int items = 0;
+      for (int o = 0; o < P.O; ++o) {
+        B.item_off[o] = items;
+        B.row_off[o] = (int)ctx->x_row_off[o];
+        items += P.S * ((P.oct[o].h + kBandRows - 1) / kBandRows);
+      }
+      B.item_off[P.O] = items;
+      B.n_items = items;
+      HIPCHK(ctx->band_cnt.ensure((size_t)items * sizeof(unsigned)));
+      HIPCHK(ctx->band_first.ensure((size_t)items * sizeof(unsigned)));
+      HIPCHK(ctx->band_start.ensure((size_t)items * sizeof(unsigned)));
+      HIPCHK(ctx->perm.ensure((size_t)cap * sizeof(unsigned)));
+      B.rowoff = ctx->rowoff.as<unsigned>();
+      B.count = ctx->band_cnt.as<unsigned>();
+      B.first = ctx->band_first.as<unsigned>();
+      B.start = ctx->band_start.as<unsigned>();
+      B.perm = ctx->perm.as<unsigned>();
+      B.cap = cap;
+      HIPCHK(launch_band_items(P, B, ctx->stream));
+      size_t tb = 0;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, B.count, ctx->band_start.as<unsigned>(), items,
+                                              ctx->stream));
+      HIPCHK(ctx->temp.ensure(tb));
+      tb = ctx->temp.bytes;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, B.count, ctx->band_start.as<unsigned>(), items,
+                                              ctx->stream));
+      HIPCHK(launch_band_fill(P, B, ctx->stream));
+      R.perm = B.perm;
+    }
     HIPCHK(launch_refine_fast(P, R, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev_heavy, ctx->stream));  // the rest is latency-bound tail work
     // Uncertain decisions exist only with fp32-rounded native planes.
@@ -1264,6 +1303,7 @@ int sift_set_candidates(sift_ctx* ctx, const sift_extremum* cand, size_t n) {
   ctx->slot_cap = (int)n;
   ctx->ext_pending = false;
   ctx->has_keep = false;
+  ctx->slots_rows = false;
   ctx->have_cand = true;
   return SIFT_OK;
 }

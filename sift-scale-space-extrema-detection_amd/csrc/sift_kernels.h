@@ -126,7 +126,28 @@ struct RefineLaunch {
   Keypoint* kp;       // per candidate (valid where status == kRefKeep)
   unsigned* uncertain;// indices for the exact pass
   unsigned* counters; // [3] n uncertain, [4] n singular
+  const unsigned* perm; // processing order: thread t refines slot perm[t] (nullptr = slot t)
 };
+
+// Processing order of the fast refinement (band_order): the slots of the
+// extrema stage are ordered (octave, scale, row, column); the refinement
+// takes them as (octave, band of kBandRows rows, scale, row, column) so the
+// candidates whose 3x3x3 patches share DoG lines of adjacent scales run
+// together (one XCD's L2) instead of a whole plane apart.
+constexpr int kBandRows = 16;
+struct BandOrder {
+  int n_oct, S, n_items;
+  int item_off[kMaxOctaves + 1];  // first item of each octave: items (band, scale) of octave o
+  int row_off[kMaxOctaves];       // first global row (o, s = 1, y = 0) of each octave in rowoff
+  const unsigned* rowoff;         // exclusive scan of the extrema stage's row counts
+  unsigned* count;                // per item: slots in it
+  unsigned* first;                // per item: its first slot
+  const unsigned* start;          // per item: exclusive scan of count (first position in the new order)
+  unsigned* perm;                 // out: position -> slot
+  int cap;
+};
+hipError_t launch_band_items(const Pyramid& P, const BandOrder& B, hipStream_t st);
+hipError_t launch_band_fill(const Pyramid& P, const BandOrder& B, hipStream_t st);
 
 size_t gauss_lds_bytes(const Pyramid& P, int o, bool fused = false);
 // Octave o can run with its extrema decisions fused (GaussLaunch.fuse):

@@ -274,7 +274,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const int n = (int)min(*L.n, (unsigned)L.cap);
   const int nb = (n + 255) / 256;
   if ((int)blockIdx.x >= nb) return;  // whole block past the live slots
-  const int i = (SIFT_REFINE_XCD ? xcd_block(blockIdx.x, nb) : (int)blockIdx.x) * 256 + threadIdx.x;
+  const int t = (SIFT_REFINE_XCD ? xcd_block(blockIdx.x, nb) : (int)blockIdx.x) * 256 + threadIdx.x;
+  const int i = (L.perm && t < n) ? min((int)L.perm[t], n - 1) : t;
   bool unc = false, polish = false;
   if (i < n && L.keep && !L.keep[i]) {
     L.status[i] = kRefDiscard;
@@ -553,6 +554,44 @@ hipError_t launch_merge_blocks(const Keypoint* in, const long long* seg, const l
 hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_decode_origins, dim3((n + 255) / 256), dim3(256), 0, st, P, keys, n, out);
+  return hipGetLastError();
+}
+
+// Band order items: one thread per (octave, band, scale) item, its slot
+// range from the row offsets of the extrema stage.
+__global__ __launch_bounds__(256) void k_band_items(const Pyramid P, const BandOrder B) {
+  const int it = blockIdx.x * 256 + threadIdx.x;
+  if (it >= B.n_items) return;
+  int o = 0;
+  while (o + 1 < B.n_oct && it >= B.item_off[o + 1]) ++o;
+  const int loc = it - B.item_off[o];
+  const int b = loc / B.S, s = loc % B.S + 1;
+  const int h = P.oct[o].h;
+  const int y0 = b * kBandRows, y1 = min(h, y0 + kBandRows);
+  const int r0 = B.row_off[o] + (s - 1) * h + y0;
+  const unsigned f = B.rowoff[r0];
+  B.first[it] = f;
+  B.count[it] = B.rowoff[r0 + (y1 - y0)] - f;
+}
+
+// One wave per item: its slots in order at its position of the new order.
+__global__ __launch_bounds__(256) void k_band_fill(const Pyramid P, const BandOrder B) {
+  const int it = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (it >= B.n_items) return;
+  const unsigned c = B.count[it], f = B.first[it], st = B.start[it];
+  for (unsigned j = threadIdx.x & 63; j < c; j += 64)
+    if (st + j < (unsigned)B.cap) B.perm[st + j] = f + j;
+}
+
+hipError_t launch_band_items(const Pyramid& P, const BandOrder& B, hipStream_t st) {
+  if (B.n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_band_items, dim3((B.n_items + 255) / 256), dim3(256), 0, st, P, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_band_fill(const Pyramid& P, const BandOrder& B, hipStream_t st) {
+  if (B.n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_band_fill, dim3((B.n_items + 3) / 4), dim3(256), 0, st, P, B);
   return hipGetLastError();
 }
 
