@@ -926,6 +926,10 @@ static int extrema_finish(sift_ctx* ctx) {
     E.value = ctx->cand_val.as<double>();
     E.keep = ctx->cand_keep.as<unsigned>();
     E.cap = ctx->cand_cap;
+    // Deferred values (SIFT_DEFER_VALUES=0: gathered here, experiments): the
+    // refinement reads each candidate's plane value from its own patch.
+    static const int defer = [] { const char* e = std::getenv("SIFT_DEFER_VALUES"); return e ? std::atoi(e) : 1; }();
+    E.deferred = defer != 0;
     HIPCHK(launch_emit(P, E, ctx->stream));
   }
   if (ctx->want_low) {  // the certain low-contrast extrema, in order (same scan + emission as the candidates)
@@ -1182,6 +1186,9 @@ int sift_copy_candidates(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* 
   std::vector<double> vals(n);
   if (n) {
     HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->slots_rows)  // deferred candidate values (EmitLaunch.deferred) from the DoG planes
+      HIPCHK(launch_fill_values(ctx->P, ctx->cand_key.as<unsigned>(), ctx->cand_val.as<double>(),
+                                ctx->counters.as<unsigned>() + kCntN, (int)n, ctx->stream));
     HIPCHK(hipMemcpyAsync(keys.data(), ctx->cand_key.p, n * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(vals.data(), ctx->cand_val.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     if (ctx->has_keep)

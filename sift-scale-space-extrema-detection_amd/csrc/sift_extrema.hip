@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
       const int x = xb + b;
       if (pos < E.cap) {
         E.keys[pos] = kbase + (unsigned)x;
-        E.value[pos] = (double)Dc[x];
+        E.value[pos] = E.deferred ? __builtin_bit_cast(double, 0x7ff8000000000000ull) : (double)Dc[x];
         if (E.keep) E.keep[pos] = 1u;
       }
       ++pos;

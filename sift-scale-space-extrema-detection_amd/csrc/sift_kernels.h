@@ -99,7 +99,13 @@ struct EmitLaunch {
   double* value;
   unsigned* keep;                // nullptr: not written
   unsigned cap;                  // slots in keys/value/keep (overflow is detected by the host)
+  int deferred;                  // 1: value = NaN ("the fp32 plane value"): the refinement reads it from its
+                                 // patch, launch_fill_values before the list is copied out; no plane gather here
 };
+
+// Fills the deferred (NaN) candidate values of slots [0, *n) from the DoG planes.
+hipError_t launch_fill_values(const Pyramid& P, const unsigned* keys, double* value, const unsigned* n, int cap,
+                              hipStream_t st);
 
 struct ExactLaunch {
   const unsigned* amb_keys;      // counters[0] of them (at most amb_cap stored)

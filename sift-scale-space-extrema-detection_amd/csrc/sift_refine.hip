@@ -286,7 +286,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int h = oc.h, w = oc.w;
     const long long plane = (long long)h * w;
     const float* __restrict__ D = P.dog + oc.dog_off;
-    const double value = L.cand_val[i];
+    double value = L.cand_val[i];
+    if (value != value) value = (double)D[s * plane + (long long)m * w + n];  // deferred: the fp32 plane value
     const double dval = EXACT ? 0.0 : fabs(value) * 0x1p-24;
     int status = kRefDiscard;
     double d[27];
@@ -554,6 +555,27 @@ hipError_t launch_merge_blocks(const Keypoint* in, const long long* seg, const l
 hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_decode_origins, dim3((n + 255) / 256), dim3(256), 0, st, P, keys, n, out);
+  return hipGetLastError();
+}
+
+// Deferred candidate values (EmitLaunch.deferred): the fp32 plane value of
+// every slot still holding the NaN marker.
+__global__ __launch_bounds__(256) void k_fill_values(const Pyramid P, const unsigned* __restrict__ keys,
+                                                     double* __restrict__ value, const unsigned* n, int cap) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int)min(*n, (unsigned)cap)) return;
+  const double v = value[i];
+  if (v == v) return;
+  int o, s, y, x;
+  decode_key(P, keys[i], o, s, y, x);
+  const Octave& oc = P.oct[o];
+  value[i] = (double)P.dog[oc.dog_off + (long long)s * oc.h * oc.w + (long long)y * oc.w + x];
+}
+
+hipError_t launch_fill_values(const Pyramid& P, const unsigned* keys, double* value, const unsigned* n, int cap,
+                              hipStream_t st) {
+  if (cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_values, dim3((cap + 255) / 256), dim3(256), 0, st, P, keys, value, n, cap);
   return hipGetLastError();
 }
 
