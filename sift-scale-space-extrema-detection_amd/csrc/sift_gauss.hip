@@ -1212,7 +1212,8 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
   // value; default all).  Measured (4K, O=4, S=5): isolated pass 0.748 ->
   // 0.730 ms, pipelined bench +0.5-1 % (tools/gpu_envab.sh).
   static const int xband = [] { const char* e = std::getenv("SIFT_XCD_BAND"); return e ? std::atoi(e) : -1; }();
-  L.xcd_band = L.o >= 1 && ((xband >> (L.o - 1)) & 1);
+  static const int xband0 = [] { const char* e = std::getenv("SIFT_XCD_BAND0"); return e ? std::atoi(e) : 0; }();
+  L.xcd_band = L.o >= 1 ? ((xband >> (L.o - 1)) & 1) : xband0;
   const dim3 grid(L.gx * L.gy * L.G);
   const size_t lds = gauss_lds_bytes(P, L.o, L.fuse != 0);
   static bool attr_set = false;

@@ -140,7 +140,10 @@ struct RefineLaunch {
 // takes them as (octave, band of kBandRows rows, scale, row, column) so the
 // candidates whose 3x3x3 patches share DoG lines of adjacent scales run
 // together (one XCD's L2) instead of a whole plane apart.
-constexpr int kBandRows = 16;
+#ifndef SIFT_BAND_ROWS
+#define SIFT_BAND_ROWS 16
+#endif
+constexpr int kBandRows = SIFT_BAND_ROWS;
 struct BandOrder {
   int n_oct, S, n_items;
   int item_off[kMaxOctaves + 1];  // first item of each octave: items (band, scale) of octave o
