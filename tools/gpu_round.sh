@@ -21,13 +21,15 @@ timeout -k 10 300 python bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err || {
 cat $O/bench_$TAG.json
 cd /tmp
 echo "[$(date +%T)] kernel trace"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench_prof_$TAG.json 2> $O/prof_$TAG.err || { echo "trace failed"; tail -5 $O/prof_$TAG.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --sustain-s 0 > $O/bench_prof_$TAG.json 2> $O/prof_$TAG.err || { echo "trace failed"; tail -5 $O/prof_$TAG.err; exit 1; }
 echo "[$(date +%T)] kernel trace, --overlap none (isolated kernels)"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_iso -o run -- python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --overlap none --inflight 2 > $O/bench_prof_${TAG}_iso.json 2> $O/prof_${TAG}_iso.err || { echo "trace failed"; tail -5 $O/prof_${TAG}_iso.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${TAG}_iso -o run -- python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --sustain-s 0 --overlap none --inflight 2 > $O/bench_prof_${TAG}_iso.json 2> $O/prof_${TAG}_iso.err || { echo "trace failed"; tail -5 $O/prof_${TAG}_iso.err; exit 1; }
 i=0
 for C in FETCH_SIZE WRITE_SIZE "TA_TA_BUSY_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1)); N=(FETCH_SIZE WRITE_SIZE TA); N=${N[$((i-1))]}
   echo "[$(date +%T)] pmc $C"
-  timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${TAG}_$N -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> $O/pmc_${TAG}_$N.err || { echo "pmc $C failed"; tail -5 $O/pmc_${TAG}_$N.err; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/pmc_${TAG}_$N -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --sustain-s 0 > /dev/null 2> $O/pmc_${TAG}_$N.err || { echo "pmc $C failed"; tail -5 $O/pmc_${TAG}_$N.err; exit 1; }
 done
+echo "[$(date +%T)] pmc SQ instruction counts (optional)"
+timeout -s KILL 60 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_${TAG}_SQ -o run -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --sustain-s 0 > /dev/null 2> $O/pmc_${TAG}_SQ.err || { echo "pmc SQ failed (optional)"; tail -3 $O/pmc_${TAG}_SQ.err; }
 echo "[$(date +%T)] done"

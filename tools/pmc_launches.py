@@ -8,12 +8,21 @@ detection, from rocprofv3 --pmc passes, grouped by (kernel, grid).
   The optional third pass (TA_TA_BUSY_sum TCC_HIT_sum TCC_MISS_sum
   GRBM_GUI_ACTIVE) gives the TA busy fraction (TA_TA_BUSY_sum over 256 TAs x
   GRBM_GUI_ACTIVE / 8 cycles) and the L2 hit rate.
+  The optional fourth pass (SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_LDS
+  SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE) gives the fp64 FMA issue
+  fraction: a wave64 v_fma_f64 occupies its SIMD 4 cycles (78.6 TFLOP/s fp64
+  vector peak = 1024 SIMDs x 16 lanes x 2 x 2.4 GHz), so fma_issue_frac =
+  4 x SQ_INSTS_VALU_FMA_F64 / (1024 x GRBM_GUI_ACTIVE / 8); valu_issue_frac
+  the same for every VALU instruction (4 cycles each, an upper estimate).
 
 The k_gauss_dog launches of one image are ordered by grid size (octave 0 has
 the largest grid); their sum is the pass's HBM traffic (`pass_hbm_bytes`),
 octave 0's is `hbm_bytes_per_launch` (bench.py reads both).
 
-usage: tools/pmc_launches.py --config-key KEY --out FILE FETCH_DIR WRITE_DIR [TA_DIR]
+The pass's traffic includes the split vertical pass (k_gauss_vert) of the
+large-radius octaves.
+
+usage: tools/pmc_launches.py --config-key KEY --out FILE FETCH_DIR WRITE_DIR [TA_DIR [SQ_DIR]]
 """
 import argparse
 import collections
@@ -23,6 +32,7 @@ import json
 import os
 
 N_TA = 256  # one texture addresser per CU
+N_SIMD = 1024  # 256 CUs x 4 SIMDs
 
 
 def collect(d):
@@ -48,9 +58,11 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("ta_dir", nargs="?")
+    ap.add_argument("sq_dir", nargs="?")
     a = ap.parse_args()
     F, Wr = collect(a.fetch_dir), collect(a.write_dir)
     T = collect(a.ta_dir) if a.ta_dir else {}
+    Q = collect(a.sq_dir) if a.sq_dir else {}
     launches = []
     for key in sorted(set(F) | set(Wr)):
         name, grid = key
@@ -69,16 +81,31 @@ def main():
         hit, miss = avg(t.get("TCC_HIT_sum", [])), avg(t.get("TCC_MISS_sum", []))
         if hit is not None and miss is not None and hit + miss > 0:
             rec["l2_hit_rate"] = hit / (hit + miss)
+        q = Q.get(key, {})
+        qgui = avg(q.get("GRBM_GUI_ACTIVE", []))
+        if qgui:
+            cyc = N_SIMD * qgui / 8.0
+            for c, k in (("SQ_INSTS_VALU_FMA_F64", "fma_issue_frac"), ("SQ_INSTS_VALU", "valu_issue_frac")):
+                v = avg(q.get(c, []))
+                if v is not None:
+                    rec[k] = 4.0 * v / cyc
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+                v = avg(q.get(c, []))
+                if v is not None:
+                    rec[c.lower()] = v
+            rec["cycles"] = qgui / 8.0
         launches.append(rec)
     gauss = sorted([r for r in launches if "k_gauss_dog" in r["kernel"]], key=lambda r: -r["grid"])
+    vert = [r for r in launches if "k_gauss_vert" in r["kernel"]]
     for o, r in enumerate(gauss):
         r["octave"] = o
     launches.sort(key=lambda r: -r["hbm_bytes"])
     out = {
         "config_key": a.config_key,
-        "pass_hbm_bytes": sum(r["hbm_bytes"] for r in gauss),
+        "pass_hbm_bytes": sum(r["hbm_bytes"] for r in gauss + vert),
         "hbm_bytes_per_launch": gauss[0]["hbm_bytes"] if gauss else None,
-        "kernel": "k_gauss_dog (octave 0); pass_hbm_bytes = all octaves' k_gauss_dog launches of one image",
+        "kernel": "k_gauss_dog (octave 0); pass_hbm_bytes = all octaves' k_gauss_dog launches of one image "
+                  "plus the split vertical pass (k_gauss_vert)",
         "launches": launches,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes, averaged per "
                   "(kernel, grid) over dispatches; bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 "
@@ -87,10 +114,12 @@ def main():
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     for r in launches:
-        print("%-44s grid %9d  %8.1f MB read %8.1f MB written%s%s" % (
+        print("%-44s grid %9d  %8.1f MB read %8.1f MB written%s%s%s%s" % (
             r["kernel"][:44], r["grid"], (r["fetch_bytes"] or 0) / 1e6, (r["write_bytes"] or 0) / 1e6,
             "  TA busy %.2f" % r["ta_busy_frac"] if "ta_busy_frac" in r else "",
-            "  L2 hit %.2f" % r["l2_hit_rate"] if "l2_hit_rate" in r else ""))
+            "  L2 hit %.2f" % r["l2_hit_rate"] if "l2_hit_rate" in r else "",
+            "  fp64 FMA issue %.2f" % r["fma_issue_frac"] if "fma_issue_frac" in r else "",
+            "  VALU issue %.2f" % r["valu_issue_frac"] if "valu_issue_frac" in r else ""))
     print("pass: %.1f MB" % (out["pass_hbm_bytes"] / 1e6))
 
 
