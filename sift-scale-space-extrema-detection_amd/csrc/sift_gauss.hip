@@ -70,6 +70,12 @@ constexpr int kUR = 16;              // radii with unrolled code (octave 0)
 #ifndef SIFT_W96
 #define SIFT_W96 1  // 96-column kernel: minimum waves per SIMD (register budget; experiments)
 #endif
+#ifndef SIFT_TW96_OPQ
+#define SIFT_TW96_OPQ 1  // 96-column kernel: per-scale opaque copies of the item map (0 with SIFT_TW96_SEQ)
+#endif
+#ifndef SIFT_TW96_SEQ
+#define SIFT_TW96_SEQ 0  // 96-column kernel: horizontal items one at a time with their epilogue (122 VGPRs, 4 waves/SIMD; measured slower: experiments)
+#endif
 #ifndef SIFT_PF96
 #define SIFT_PF96 2
 #endif
@@ -594,6 +600,40 @@ __device__ __forceinline__ void horz_full96(const GTile& T, const cdouble* wp, c
   }
 }
 
+// The same, one item at a time, each handed to epi(i, out) as soon as its
+// 4 chains are done: only one item's accumulators and reads are live
+// (SIFT_TW96_SEQ; the interleaved form keeps all three).
+template <int R, class Epi>
+__device__ __forceinline__ void horz_full96_seq(const GTile& T, const cdouble* wp, const double* V, Epi&& epi) {
+  constexpr int NP = R + 2;  // double2 pairs per row
+  constexpr int PF = kPFH;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double* rp = V + (8 * T.wv + T.irow[i]) * T.sw + 4 * T.icg[i];
+    double out[4];
+    double2 u[NP];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[q] = 0.0;
+#pragma unroll
+    for (int n2 = 0; n2 < PF && n2 < NP; ++n2) u[n2] = *reinterpret_cast<const double2*>(rp + 2 * n2);
+#pragma unroll
+    for (int n2 = 0; n2 < NP; ++n2) {
+      if (n2 + PF < NP) u[n2 + PF] = *reinterpret_cast<const double2*>(rp + 2 * (n2 + PF));
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int n = 2 * n2 + e;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = n - q;
+          if (k >= 0 && k <= 2 * R) out[q] = fma((double)wp[k], e ? u[n2].y : u[n2].x, out[q]);
+        }
+      }
+      pin(out);
+    }
+    epi(i, out);
+  }
+}
+
 __device__ __forceinline__ void horz_full_gen(const GTile& T, int r, const cdouble* wp, const double* V,
                                               double (&out)[kNR][4]) {
   const int NV = 2 * r + 4;
@@ -711,6 +751,13 @@ __device__ __forceinline__ void horz96_any_(std::integer_sequence<int, Rs...>, c
                                            const cdouble* wp, const double* V, double (&out)[3][4]) {
   bool done = false;
   ((!done && r == Rs ? (horz_full96<Rs>(T, wp, V, out), done = true) : false), ...);
+}
+
+template <class Epi, int... Rs>
+__device__ __forceinline__ void horz96s_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
+                                            const cdouble* wp, const double* V, Epi&& epi) {
+  bool done = false;
+  ((!done && r == Rs ? (horz_full96_seq<Rs>(T, wp, V, epi), done = true) : false), ...);
 }
 
 // Unrolled radii 0..RMAX.
@@ -924,9 +971,49 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
     // keeps it all live (dozens of VGPRs, half the occupancy).
     GTile Ts = T;
     asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
+#if SIFT_TW96_OPQ
     if constexpr (TW == 96) {
 #pragma unroll
       for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Ts.icg[i]), "+v"(Ts.irow[i]));
+    }
+#endif
+    if constexpr (TW == 96 && SIFT_TW96_SEQ) {
+      // one item at a time: horizontal chains, then its stores, DoG and seed
+      vert96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V);
+      wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
+      const unsigned pb = (unsigned)plane * 4u;
+      const bool stor = s >= s_begin && st;
+      const __amdgpu_buffer_rsrc_t rg =
+          __builtin_amdgcn_make_buffer_rsrc(L.gauss ? L.gauss + s * plane : L.dog, 0, pb, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rd =
+          __builtin_amdgcn_make_buffer_rsrc(L.dog + (s > 0 ? s - 1 : 0) * plane, 0, pb, 0x00020000);
+      horz96s_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V,
+                   [&](int i, const double (&o)[4]) {
+                     double d[4];
+#pragma unroll
+                     for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[q];
+                     const int y = T.y0 + 8 * T.wv + irw(i);
+                     const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
+                     if (stor) {
+                       if (L.vec) {
+                         if (L.gauss) bstore4(rg, voff[i], o);
+                         if (s > 0) bstore4(rd, voff[i], d);
+                       } else if (own[i]) {
+                         const long long pp = (long long)y * T.w + x;
+                         if (L.gauss) store4(L.gauss + s * plane + pp, o, nvalid);
+                         if (s > 0) store4(L.dog + (s - 1) * plane + pp, d, nvalid);
+                       }
+                     }
+                     if (s == P.S && L.next_seed && s >= s_begin && own[i] && !(y & 1)) {
+                       double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+                       sd[0] = o[0];
+                       if (nvalid > 2) sd[1] = o[2];
+                     }
+#pragma unroll
+                     for (int q = 0; q < 4; ++q) lprev[i][q] = o[q];
+                   });
+      wave_lds_fence();  // strip rows read before the next scale overwrites them
+      continue;
     }
     double out[NI][4];
     if constexpr (TW == 96) {
