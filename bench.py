@@ -25,6 +25,7 @@ K-step `value`).
 import argparse
 import glob
 import json
+import math
 import os
 import sys
 import time
@@ -329,19 +330,20 @@ def main():
         elapsed = float(e.item())
     # Steady state: the same pipelined loop for a few seconds (thousands of
     # images; no per-image host work beyond the settle), its own clock.
+    # The image count comes from the timed region's max-over-ranks time, so
+    # every rank runs the same number of per-image collectives.
     sustained = None
     if args.sustain_s > 0:
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
-        ns, t1 = 0, time.perf_counter()
-        while True:
+        n_sus = max(nin, int(math.ceil(args.sustain_s / max(elapsed / NI, 1e-6))))
+        t1 = time.perf_counter()
+        for ns in range(n_sus):
             launch(NI + ns)
             if ns >= nin - 1:
                 finish(NI + ns - (nin - 1), False)
-            ns += 1
-            if ns >= nin and time.perf_counter() - t1 >= args.sustain_s:
-                break
+        ns = n_sus
         flush()
         for i in range(max(0, ns - (nin - 1)), ns):
             finish(NI + i, False)
