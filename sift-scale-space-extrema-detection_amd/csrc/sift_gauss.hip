@@ -71,10 +71,11 @@ constexpr int kUR = 16;              // radii with unrolled code (octave 0)
 #define SIFT_W96 1  // 96-column kernel: minimum waves per SIMD (register budget; experiments)
 #endif
 #ifndef SIFT_TW96_OPQ
-#define SIFT_TW96_OPQ 1  // 96-column kernel: per-scale opaque copies of the item map (0 with SIFT_TW96_SEQ)
+#define SIFT_TW96_OPQ 0  // 96-column kernel: per-scale opaque copies of the item map (1 with SIFT_TW96_SEQ 0)
 #endif
 #ifndef SIFT_TW96_SEQ
-#define SIFT_TW96_SEQ 0  // 96-column kernel: horizontal items one at a time with their epilogue (122 VGPRs, 4 waves/SIMD; measured slower: experiments)
+#define SIFT_TW96_SEQ 2  // 96-column kernel: horizontal items 0-1 side by side then 2, each group with its epilogue
+                         // (122 VGPRs, 4 waves/SIMD; 1 = one at a time, 0 = all three interleaved, 138 VGPRs)
 #endif
 #ifndef SIFT_PF96
 #define SIFT_PF96 2
@@ -603,34 +604,57 @@ __device__ __forceinline__ void horz_full96(const GTile& T, const cdouble* wp, c
 // The same, one item at a time, each handed to epi(i, out) as soon as its
 // 4 chains are done: only one item's accumulators and reads are live
 // (SIFT_TW96_SEQ; the interleaved form keeps all three).
-template <int R, class Epi>
-__device__ __forceinline__ void horz_full96_seq(const GTile& T, const cdouble* wp, const double* V, Epi&& epi) {
+// Items [I0, I0 + NI) of the lane side by side (4 NI fma chains).
+template <int R, int I0, int NI, class Epi>
+__device__ __forceinline__ void horz96_group(const GTile& T, const cdouble* wp, const double* V, Epi&& epi) {
   constexpr int NP = R + 2;  // double2 pairs per row
   constexpr int PF = kPFH;
+  const double* rp[NI];
+  double out[NI][4];
+  double2 u[NI][NP];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double* rp = V + (8 * T.wv + T.irow[i]) * T.sw + 4 * T.icg[i];
-    double out[4];
-    double2 u[NP];
+  for (int j = 0; j < NI; ++j) {
+    rp[j] = V + (8 * T.wv + T.irow[I0 + j]) * T.sw + 4 * T.icg[I0 + j];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[q] = 0.0;
+    for (int q = 0; q < 4; ++q) out[j][q] = 0.0;
+  }
 #pragma unroll
-    for (int n2 = 0; n2 < PF && n2 < NP; ++n2) u[n2] = *reinterpret_cast<const double2*>(rp + 2 * n2);
+  for (int n2 = 0; n2 < PF && n2 < NP; ++n2)
 #pragma unroll
-    for (int n2 = 0; n2 < NP; ++n2) {
-      if (n2 + PF < NP) u[n2 + PF] = *reinterpret_cast<const double2*>(rp + 2 * (n2 + PF));
+    for (int j = 0; j < NI; ++j) u[j][n2] = *reinterpret_cast<const double2*>(rp[j] + 2 * n2);
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int n = 2 * n2 + e;
+  for (int n2 = 0; n2 < NP; ++n2) {
+    if (n2 + PF < NP)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int k = n - q;
-          if (k >= 0 && k <= 2 * R) out[q] = fma((double)wp[k], e ? u[n2].y : u[n2].x, out[q]);
-        }
+      for (int j = 0; j < NI; ++j) u[j][n2 + PF] = *reinterpret_cast<const double2*>(rp[j] + 2 * (n2 + PF));
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * n2 + e;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = n - q;
+        if (k >= 0 && k <= 2 * R)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) out[j][q] = fma((double)wp[k], e ? u[j][n2].y : u[j][n2].x, out[j][q]);
       }
-      pin(out);
     }
-    epi(i, out);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) pin(out[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) epi(I0 + j, out[j]);
+}
+
+// SIFT_TW96_SEQ 1: items one at a time; 2: items 0-1 side by side, then 2.
+template <int R, class Epi>
+__device__ __forceinline__ void horz_full96_seq(const GTile& T, const cdouble* wp, const double* V, Epi&& epi) {
+  if constexpr (SIFT_TW96_SEQ == 2) {
+    horz96_group<R, 0, 2>(T, wp, V, epi);
+    horz96_group<R, 2, 1>(T, wp, V, epi);
+  } else {
+    horz96_group<R, 0, 1>(T, wp, V, epi);
+    horz96_group<R, 1, 1>(T, wp, V, epi);
+    horz96_group<R, 2, 1>(T, wp, V, epi);
   }
 }
 
