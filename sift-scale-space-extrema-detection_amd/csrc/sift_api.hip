@@ -972,6 +972,18 @@ static int extrema_finish(sift_ctx* ctx) {
   X.keep = ctx->cand_keep.as<unsigned>();
   X.value = ctx->cand_val.as<double>();
   X.counters = cnt;
+  static const int xpos = [] { const char* e = std::getenv("SIFT_XPOS"); return e ? std::atoi(e) : 1; }();
+  if (xpos) {  // list positions from the emission geometry instead of a binary search
+    X.bitmap = ctx->bitmap.as<unsigned long long>();
+    X.rowoff = ctx->rowoff.as<unsigned>();
+    for (int o = 0; o < P.O; ++o) {
+      X.row_off[o] = (int)ctx->x_row_off[o];
+      X.word_off[o] = ctx->x_word_off[o];
+      X.nw[o] = ctx->x_nw[o];
+      X.ww[o] = ctx->x_ww[o];
+      X.woff[o] = ctx->x_woff[o];
+    }
+  }
   HIPCHK(launch_exact_extrema(P, X, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->slot_cap = (int)ctx->cand_cap;

@@ -284,15 +284,32 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
   const unsigned n = min(*X.n, X.cap);
   for (unsigned j = blockIdx.x; j < n_amb; j += gridDim.x) {
     const unsigned key = X.amb_keys[j];
-    // position of key in the ordered candidate list (binary search)
-    unsigned lo = 0, hi = n;
-    while (lo < hi) {
-      const unsigned mid = (lo + hi) >> 1;
-      if (X.keys[mid] < key) lo = mid + 1; else hi = mid;
-    }
-    const unsigned idx = lo;
     int o, s, y, x;
     decode_key(P, key, o, s, y, x);
+    // position of key in the ordered candidate list
+    unsigned idx;
+    if (X.bitmap) {  // the row's offset + the candidate bits before x (parallel loads, one wave reduction)
+      const int h = P.oct[o].h;
+      const int rr = (s - 1) * h + y;
+      const long long wbase = X.word_off[o] + (long long)rr * X.nw[o];
+      const int xr = x - X.woff[o], xw = xr / X.ww[o], b = xr - xw * X.ww[o];
+      unsigned c = 0;
+      for (int w = (int)threadIdx.x; w <= xw; w += 64) {
+        unsigned long long word = X.bitmap[wbase + w];
+        if (w == xw) word &= (1ull << b) - 1ull;
+        c += (unsigned)__popcll(word);
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+      idx = X.rowoff[X.row_off[o] + rr] + c;
+    } else {  // binary search
+      unsigned lo = 0, hi = n;
+      while (lo < hi) {
+        const unsigned mid = (lo + hi) >> 1;
+        if (X.keys[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      idx = lo;
+    }
     double* d27 = smem;
     double* Lbuf = smem + 32;
     double* sh = smem + 32 + 40;

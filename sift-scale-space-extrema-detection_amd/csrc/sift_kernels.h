@@ -118,6 +118,14 @@ struct ExactLaunch {
   unsigned* counters;            // [6]: late low-contrast extrema (ambiguous ones decided low)
   unsigned* late_keys;           // their keys / exact values (nullptr = not listed), amb_cap slots
   double* late_vals;
+  // Emission geometry (EmitLaunch): a key's list position is its row's offset
+  // plus the candidate bits before it in the row's bitmap words (bitmap ==
+  // nullptr: binary search over keys).
+  const unsigned long long* bitmap;
+  const unsigned* rowoff;
+  int row_off[kMaxOctaves];
+  long long word_off[kMaxOctaves];
+  int nw[kMaxOctaves], ww[kMaxOctaves], woff[kMaxOctaves];
 };
 
 struct RefineLaunch {
