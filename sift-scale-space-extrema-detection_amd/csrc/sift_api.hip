@@ -325,6 +325,7 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
   if (W < 1 || H < 1) return set_err(ctx, SIFT_E_ARG, "empty image");
   const int O = p->num_octaves, S = p->scales_per_octave, NS = S + 3, ND = S + 2;
   ctx->p = *p;
+  ctx->scan_first = 0;
   ctx->W = W;
   ctx->H = H;
   ctx->dims.assign(2 * O, 0);
@@ -751,6 +752,7 @@ int sift_load_dog(sift_ctx* ctx, const float* planes, int width, int height, con
   ctx->P.seeds = nullptr;
   ctx->dog_source = kForeign;
   ctx->o_first = 0;
+  ctx->scan_first = 0;
   ctx->have_gauss = false;
   ctx->have_cand = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -779,6 +781,7 @@ int sift_load_scale_space(sift_ctx* ctx, const float* planes, int width, int hei
   ctx->P.seeds = nullptr;
   ctx->dog_source = kForeign;
   ctx->o_first = 0;
+  ctx->scan_first = 0;
   ctx->have_gauss = true;
   ctx->have_cand = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));

@@ -41,8 +41,10 @@ function lastOf(type) {
 
 function writePlanes(prefix, pyramid) {
   // Each plane as fp64 little-endian, concatenated octave-major.
+  // Written plane by plane: a 4K pyramid (2.8 GB) exceeds Node 12's
+  // largest Buffer.
   const meta = [];
-  const chunks = [];
+  const fd = fs.openSync(path.join(outDir, prefix + '.f64'), 'w');
   for (let o = 0; o < pyramid.length; o++) {
     const om = [];
     for (let s = 0; s < pyramid[o].length; s++) {
@@ -50,12 +52,12 @@ function writePlanes(prefix, pyramid) {
       const h = img.length, w = img[0].length;
       const buf = new Float64Array(h * w);
       for (let y = 0; y < h; y++) for (let x = 0; x < w; x++) buf[y * w + x] = img[y][x];
-      chunks.push(Buffer.from(buf.buffer));
+      fs.writeSync(fd, Buffer.from(buf.buffer));
       om.push({ blurLevel: pyramid[o][s].blurLevel, h: h, w: w });
     }
     meta.push(om);
   }
-  fs.writeFileSync(path.join(outDir, prefix + '.f64'), Buffer.concat(chunks));
+  fs.closeSync(fd);
   return meta;
 }
 

@@ -455,3 +455,29 @@ def test_owned_rows_and_block_counts(gpu_ctx):
         keep = _owned(org, lo, hi, hi < 0)
         assert kp.tobytes() == whole[keep].tobytes()
         np.testing.assert_array_equal(counts, np.bincount(org[keep, 0] * S + org[keep, 1] - 1, minlength=O * S))
+
+
+def test_loaded_dog_after_range_detection_scans_every_octave(gpu_ctx):
+    """A context that ran sift_detect_from_seed_range_device (which scans only
+    octaves >= its octave_scan_first) and then loads a caller DoG pyramid
+    scans every octave of the loaded pyramid, as a fresh context does (ADVICE
+    r2: the load paths reset the scan range)."""
+    import torch
+    W, H, O, S = 256, 192, 4, 3
+    img = blob_image(W, H, seed=11)
+    p = sift_amd.make_params(O, S)
+    gpu_ctx.build_scale_space(img, p)
+    planes = np.concatenate([gpu_ctx.plane(sift_amd.PLANE_DOG, o, s).ravel()
+                             for o in range(O) for s in range(S + 2)])
+    h1, w1 = gpu_ctx.dims(1)
+    seed = torch.tensor(gpu_ctx.plane(sift_amd.PLANE_GAUSS, 1, 0).astype(np.float64), device="cuda:0")
+    gpu_ctx.detect_from_seed_range_device(seed.data_ptr(), 1, 3, W, H, p)
+    torch.cuda.synchronize()
+    gpu_ctx.load_dog(planes, W, H, p)
+    cand, low = gpu_ctx.find_extrema()
+    with sift_amd.Context() as fresh:
+        fresh.load_dog(planes, W, H, p)
+        cref, lref = fresh.find_extrema()
+    assert set(np.unique(cref["octave"]).tolist()) >= {0, 1}
+    np.testing.assert_array_equal(cand, cref)
+    assert low == lref
