@@ -328,6 +328,10 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    # What the timed region computed: the keypoint records of its last image
+    # (the pipelined own-stream schedule), checked after the measurements
+    # against a synchronous detection of the same input on a fresh context.
+    kp_timed = ctxs[(NI - 1) % nin].keypoints().tobytes()
     # Steady state: the same pipelined loop for a few seconds (thousands of
     # images; no per-image host work beyond the settle), its own clock.
     # The image count comes from the timed region's max-over-ranks time, so
@@ -372,6 +376,12 @@ def main():
             iso[k] += t[k] / n_iso
         for o, v in enumerate(ctx.octave_timings()):
             iso_oct[o] += v / n_iso
+    with sift_amd.Context(dev) as vctx:
+        vctx.detect_device(d_img.data_ptr(), W, H, params)
+        verified = vctx.keypoints().tobytes() == kp_timed
+    if not verified:
+        print("bench.py: rank %d: the timed region's last keypoint list differs from a synchronous detection"
+              % rank, file=sys.stderr)
     K = args.steps
     Bt = max(1, args.batch)
     ms_per_step = elapsed / K * 1e3
@@ -424,6 +434,10 @@ def main():
             "keypoints": counts["keypoints"],
             "candidates": counts["candidates"],
             "keypoints_all_ranks": n_total,
+            "verified": verified,
+            "verified_what": ("rank 0: the last timed image's keypoint records (pipelined schedule, %d contexts) "
+                              "byte-identical to a synchronous sift_detect_device of the same input on a fresh "
+                              "context" % nin),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "Gaussian+DoG pass: k_gauss_dog, %d launches (one per octave)" % O,

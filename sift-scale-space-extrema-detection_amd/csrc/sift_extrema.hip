@@ -388,13 +388,20 @@ hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st) {
 }
 
 size_t exact_lds_bytes(const Pyramid& P) {
+  // octaves with kept fp64 planes (l64) read their patches, no scratch
   int rmax = 0;
-  for (int o = 0; o < P.O; ++o) rmax = std::max(rmax, P.oct[o].rmax);
+  for (int o = 0; o < P.O; ++o)
+    if (P.oct[o].l64_off < 0) rmax = std::max(rmax, P.oct[o].rmax);
   return sizeof(double) * (size_t)(32 + 40 + exact_scratch_doubles(rmax));
 }
 
 hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, hipStream_t st) {
   const unsigned grid = std::max(1u, std::min(X.amb_cap, 4096u));
+  static const bool attr = [] {  // scratch of radii above ~335 exceeds 64 KiB
+    (void)hipFuncSetAttribute((const void*)k_exact_extrema, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
   hipLaunchKernelGGL(k_exact_extrema, dim3(grid), dim3(64), exact_lds_bytes(P), st, P, X);
   return hipGetLastError();
 }

@@ -77,6 +77,9 @@ constexpr int kUR = 16;              // radii with unrolled code (octave 0)
 #define SIFT_TW96_SEQ 2  // 96-column kernel: horizontal items 0-1 side by side then 2, each group with its epilogue
                          // (122 VGPRs, 4 waves/SIMD; 1 = one at a time, 0 = all three interleaved, 138 VGPRs)
 #endif
+#ifndef SIFT_B128MAP
+#define SIFT_B128MAP 1  // 96-column kernel: conflict-free ds_read_b128 item map (b128_group)
+#endif
 #ifndef SIFT_PF96
 #define SIFT_PF96 2
 #endif
@@ -116,6 +119,21 @@ struct GTile {
   const double* S0;    // octave 0: staged input region [..][kBW0]
   __amdgpu_buffer_rsrc_t rsrc;  // o >= 1 (or materialised octave 0): fp64 base plane h x w
 };
+
+// ds_read_b128 serves a wave in four 16-lane groups, {0-3,12-15,20-27},
+// {4-11,16-19,28-31} and the same +32; lane -> (group, position in group).
+__device__ __forceinline__ void b128_group(int lane, int& g, int& j) {
+  const int l = lane & 31;
+  int ga, ja;
+  if (l < 4) ga = 0, ja = l;
+  else if (l < 12) ga = 1, ja = l - 4;
+  else if (l < 16) ga = 0, ja = l - 8;
+  else if (l < 20) ga = 1, ja = l - 8;
+  else if (l < 28) ga = 0, ja = l - 12;
+  else ga = 1, ja = l - 16;
+  g = 2 * (lane >> 5) + ga;
+  j = ja;
+}
 
 // Register pinning: an empty asm that reads and writes the accumulators and
 // clobbers memory.  The compiler keeps the source order of the fma chains
@@ -423,7 +441,8 @@ __device__ __forceinline__ void vert_glob_gen(const GTile& T, int r, const cdoub
 __global__ __launch_bounds__(256) void k_gauss_vert(const Pyramid P, int o, const double* __restrict__ base,
                                                     double* __restrict__ vout) {
   const Octave& oc = P.oct[o];
-  const int s = blockIdx.z;
+  // largest radius (longest chains) first: blocks are dispatched in z order
+  const int s = (int)gridDim.z - 1 - (int)blockIdx.z;
   const int r = oc.rad[s], h = oc.h, w = oc.w;
   const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -920,12 +939,22 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
   T.cg = T.lane & (kCG - 1);
   T.rs = T.lane / kCG;
   if constexpr (TW == 96) {
+#if SIFT_B128MAP
+    int g, j;  // conflict-free ds_read_b128 item map (k_gauss_lds)
+    b128_group(T.lane, g, j);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      T.icg[i] = 8 * i + (j & 7);
+      T.irow[i] = 2 * g + (j >> 3);
+    }
+#else
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int idx = T.lane + 64 * i;
       T.icg[i] = idx % 24;
       T.irow[i] = idx / 24;
     }
+#endif
   }
   // item i of the lane: wave row irw(i), first column x0 + 4 icg(i)
   auto irw = [&](int i) { return TW == kGX ? T.rs + kRS * i : T.irow[i]; };
@@ -1139,6 +1168,272 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-resident base (octaves >= 1 whose base region and strip fit one CU's
+// LDS: 4K / 8K octaves 1 and 2).  k_gauss_dog's octaves >= 1 re-read the
+// base region from L1/L2 once per SCALE: S+3 passes of 16-byte loads whose
+// address processing bounds the launch (TA busy 0.6-0.8), and every scale's
+// first load waits behind the previous scale's plane stores (vmcnt counts
+// loads and stores in issue order).  Here a block owns a TW x 64 tile with 8
+// waves (8 rows each), stages the fp64 base region (64 + 2R rows x TW + 2R
+// columns, edges replicated) in LDS ONCE, and every scale's vertical pass
+// reads it from LDS: no global load after the staging, stores fire and
+// forget.  The price is occupancy (one block = 2 waves per SIMD), paid back
+// with registers: up to 256 VGPRs per lane, so deeper prefetch and more
+// independent fma chains per wave.  Same fma chains per output as the tile
+// kernel (bit-identical planes).
+// ---------------------------------------------------------------------------
+constexpr int kLY = 64;   // tile rows (8 waves x 8)
+constexpr int kLPF = 8;   // LDS rows in flight, vertical pass
+
+// Strip columns c = lane and lane + 64 of the wave's 8 rows for radius R,
+// from the staged region B (row stride BW, region row 0 = tile row -Rm,
+// region column 0 = tile column -Rm): V[t][c] = sum_k w_k B[8 wv + t + k +
+// d][c + d], d = Rm - R.  One double per lane and row: 64 consecutive
+// doubles per ds_read_b64, conflict-free (a 16-byte pair per lane is 8-byte
+// aligned when d is odd: ds_read2_b64 with 2-way conflicts); every row of the
+// window at an immediate offset from one address.
+template <int R, int TW, int BW>
+__device__ __forceinline__ void vert_lds(const GTile& T, int d, const double* B, const cdouble* wp, double* V) {
+  constexpr int NC = TW + 2 * R;
+  constexpr bool TWO = NC > 64;
+  static_assert(NC <= 128, "two columns per lane");
+  constexpr int NJ = 2 * R + 8;
+  constexpr int PF = NJ < kLPF ? NJ : kLPF;
+  if (!TWO && T.lane >= NC) return;
+  const double* src = B + (8 * T.wv + d) * BW + d + T.lane;
+  double a0[8], a1[8];
+  double2 v[NJ];
+  auto ld = [&](int j) -> double2 { return make_double2(src[j * BW], TWO ? src[j * BW + 64] : 0.0); };
+#pragma unroll
+  for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
+#pragma unroll
+  for (int j = 0; j < PF; ++j) v[j] = ld(j);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (j + PF < NJ) v[j + PF] = ld(j + PF);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int k = j - t;
+      if (k >= 0 && k <= 2 * R) {
+        a0[t] = fma((double)wp[k], v[j].x, a0[t]);
+        if (TWO) a1[t] = fma((double)wp[k], v[j].y, a1[t]);
+      }
+    }
+    pin(a0);
+    if (TWO) pin(a1);
+  }
+  double* Vw = V + 8 * T.wv * T.sw + T.lane;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) Vw[t * T.sw] = a0[t];
+  if (TWO && T.lane + 64 < NC)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) Vw[t * T.sw + 64] = a1[t];
+}
+
+// Generic radii (up to 32): the 8-row chunks over zero-padded taps of
+// vert_glob_gen (same fma chains), rows from the staged region.
+template <int TW, int BW>
+__device__ __forceinline__ void vert_lds_gen(const GTile& T, int r, int d, const double* B, const cdouble* wp,
+                                             double* V) {
+  const int NC = TW + 2 * r, NJ = 2 * r + 8;
+  const double* src = B + (8 * T.wv + d) * BW + d + T.lane;
+  const bool two = T.lane + 64 < NC;
+  double a0[8], a1[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
+  auto chunk = [&](int jb, auto C, auto first) {
+    using CC = decltype(C);
+    double2 v[8];
+#pragma unroll
+    for (int k = 0; k < CC::kRows; ++k) v[k] = make_double2(src[(jb + k) * BW], src[(jb + k) * BW + 64]);
+    const cdouble* w = wp + jb;
+    CC::template run<decltype(first)::value>([&](int k, int t) {
+      a0[t] = fma((double)w[k - t], v[k].x, a0[t]);
+      a1[t] = fma((double)w[k - t], v[k].y, a1[t]);
+    });
+    pin(a0);
+    pin(a1);
+  };
+  vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
+  for (int jb = 8; jb < NJ; jb += 8)
+    vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
+  double* Vw = V + 8 * T.wv * T.sw + T.lane;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) Vw[t * T.sw] = a0[t];
+  if (two)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) Vw[t * T.sw + 64] = a1[t];
+}
+
+template <int TW, int BW, int... Rs>
+__device__ __forceinline__ void vert_lds_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r, int d,
+                                             const double* B, const cdouble* wp, double* V) {
+  bool done = false;
+  ((!done && r == Rs ? (vert_lds<Rs, TW, BW>(T, d, B, wp, V), done = true) : false), ...);
+  if (!done) vert_lds_gen<TW, BW>(T, r, d, B, wp, V);
+}
+
+// Region row stride (doubles) of the staged base: TW + 2 Rc columns, Rc the
+// largest octave radius the instance takes (12 for 96-column tiles, whose
+// radii are all unrolled; 23 for 64-column tiles: 4K / 8K octave 2 at S = 5),
+// so every row of a window is an immediate offset.
+__host__ __device__ constexpr int lds_region_stride(int tw) { return tw == 96 ? 96 + 2 * 12 : 64 + 2 * 23; }
+
+template <int TW, int RMAX>
+__global__ __launch_bounds__(512) void k_gauss_lds(const Pyramid P, const GaussLaunch L) {
+  constexpr int BW = lds_region_stride(TW);
+  constexpr int NI = TW == kGX ? kNR : 3;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Octave& oc = P.oct[L.o];
+  int lb = blockIdx.x;
+  if (L.xcd_band) {
+    const int nb = L.gx * L.gy * L.G, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    lb = xc * q + min(xc, rm) + (lb >> 3);
+  }
+  const int bz = lb % L.G, bt = lb / L.G;
+  const int bx = bt % L.gx, by = bt / L.gx;
+  GTile T;
+  T.bx = bx;
+  T.h = oc.h;
+  T.w = oc.w;
+  T.x0 = bx * TW;
+  T.y0 = by * kLY;
+  T.lane = threadIdx.x & 63;
+  T.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  T.cg = T.lane & (kCG - 1);
+  T.rs = T.lane / kCG;
+  if constexpr (TW == 96) {
+    // item i of lane (group g, position j): columns 4 (8 i + j % 8) .. + 3
+    // of wave row 2 g + j / 8 -- in every 16-lane group of a ds_read_b128
+    // the 8 column groups of two adjacent rows (strip stride 2 mod 4
+    // doubles): 16 distinct bank quads, conflict-free.
+    int g, j;
+    b128_group(T.lane, g, j);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      T.icg[i] = 8 * i + (j & 7);
+      T.irow[i] = 2 * g + (j >> 3);
+    }
+  }
+  auto irw = [&](int i) { return TW == kGX ? T.rs + kRS * i : T.irow[i]; };
+  auto icg = [&](int i) { return TW == kGX ? T.cg : T.icg[i]; };
+  T.sw = L.sw;
+  const int Rm = oc.rmax;
+  constexpr int bw = BW;
+  double* V = smem;
+  double* B = smem + kLY * T.sw;
+
+  if (L.zero)
+    for (int i = threadIdx.x; i < kLY * T.sw; i += 512) smem[i] = 0.0;
+  {
+    // Stage base rows y0 - Rm .. y0 + 63 + Rm, columns x0 - Rm .. x0 + TW +
+    // Rm - 1, clamped (replicate edges): one 16-byte load per column pair
+    // (pair x, x+1 read at clamp(x, 0, w-2), edge pairs selected as in
+    // vert_glob2), all of a wave's rows in flight before its LDS writes.
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L.base), 0, T.h * T.w * 8, 0x00020000);
+    const int nrr = kLY + 2 * Rm, npair = (TW + 2 * Rm) / 2;
+    const int x = T.x0 - Rm + 2 * T.lane;
+    const int xoff = clampi(x, 0, T.w - 2) * 8;
+    const bool lo_edge = x < 0, hi_edge = x >= T.w - 1;
+    constexpr int kMaxRows = (kLY + 2 * 32 + 7) / 8;  // region rows per wave (radii up to 32)
+    double2 v[kMaxRows];
+    if (T.lane < npair) {
+#pragma unroll
+      for (int i = 0; i < kMaxRows; ++i) {
+        const int rr = T.wv + 8 * i;
+        if (rr < nrr) {
+          const int yy = clampi(T.y0 - Rm + rr, 0, T.h - 1);
+          v[i] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, xoff, yy * T.w * 8, 0));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kMaxRows; ++i) {
+        const int rr = T.wv + 8 * i;
+        if (rr < nrr)
+          *reinterpret_cast<double2*>(B + rr * bw + 2 * T.lane) =
+              make_double2(hi_edge ? v[i].y : v[i].x, lo_edge ? v[i].x : v[i].y);
+      }
+    }
+  }
+  const long long plane = (long long)T.h * T.w;
+  bool own[NI];
+  int voff[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int y = T.y0 + 8 * T.wv + irw(i);
+    const int x = T.x0 + 4 * icg(i);
+    own[i] = y < T.h && T.w - x > 0;
+    voff[i] = own[i] ? (y * T.w + x) * 4 : 0x7ffffff0;
+  }
+  const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
+  const int s_first = max(0, s_begin - 1);
+  __syncthreads();  // staged region / zeroed strip visible to every wave
+
+  const bool st = !(L.dbg & 1);
+  double lprev[NI][4];
+  for (int s = s_first; s < s_end; ++s) {
+    const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+    GTile Ts = T;
+    asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
+    const int r = oc.rad[s];
+    vert_lds_any_<TW, BW>(std::make_integer_sequence<int, RMAX + 1>{}, Ts, r, Rm - r, B, wp, V);
+    wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
+    double out[NI][4];
+    if constexpr (TW == 96) horz96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, r, wp, V, out);
+    else horz_any<false, RMAX>(Ts, r, wp, V, out);
+    wave_lds_fence();  // strip rows read before the next scale overwrites them
+    double d[NI][4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
+    if (s >= s_begin && (st || out[0][0] == 12345.0)) {
+      if (L.vec) {
+        const unsigned pb = (unsigned)plane * 4u;
+        if (L.gauss) {
+          const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L.gauss + s * plane, 0, pb, 0x00020000);
+#pragma unroll
+          for (int i = 0; i < NI; ++i) bstore4(rg, voff[i], out[i]);
+        }
+        if (s > 0) {
+          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L.dog + (s - 1) * plane, 0, pb, 0x00020000);
+#pragma unroll
+          for (int i = 0; i < NI; ++i) bstore4(rd, voff[i], d[i]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int y = T.y0 + 8 * T.wv + irw(i);
+          const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
+          if (own[i]) {
+            const long long pp = (long long)y * T.w + x;
+            if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
+            if (s > 0) store4(L.dog + (s - 1) * plane + pp, d[i], nvalid);
+          }
+        }
+      }
+    }
+    if (s == P.S && L.next_seed && s >= s_begin) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int y = T.y0 + 8 * T.wv + irw(i);
+        const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
+        if (own[i] && !(y & 1)) {
+          double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+          sd[0] = out[i][0];
+          if (nvalid > 2) sd[1] = out[i][2];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
+  }
+}
+
 // Materialised octave-0 base (fp64), for octave-0 radii beyond kUR.
 __global__ __launch_bounds__(256) void k_upsample_base(const Pyramid P, double* __restrict__ b) {
   const int h = P.oct[0].h, w = P.oct[0].w;
@@ -1282,8 +1577,12 @@ static int scale_groups(const Pyramid& P, int o) {
   const Octave& oc = P.oct[o];
   const int tw = tile_w(P, o);
   const long long tiles = (long long)((oc.w + tw - 1) / tw) * ((oc.h + kGY - 1) / kGY);
+  // Split-pass octaves recompute only the horizontal pass of the scale
+  // before a group: split them until ~8 waves per SIMD (their chains are
+  // latency-bound at radius 47+).
+  const long long target = gauss_vsplit(P, o) ? 2048 : 400;
   int g = 1;
-  while (g < P.NS && tiles * g < 400) ++g;
+  while (g < P.NS && tiles * g < target) ++g;
   return g;
 }
 
@@ -1291,6 +1590,20 @@ template <bool O0, int SWC, int RMAX, bool XF>
 static void set_attr() {
   (void)hipFuncSetAttribute((const void*)k_gauss_dog<O0, SWC, RMAX, XF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
+}
+
+// LDS-resident path (k_gauss_lds): bytes of the strip (64 rows) + staged
+// region, 0 when octave o does not take it (octave 0, split pass, fp64
+// planes kept, planes narrower than 2 columns, region wider than 128
+// columns, or more than the CU's 160 KiB).  SIFT_GAUSS_LDS=0 turns it off
+// (A/B against k_gauss_dog).
+static size_t lds_path_bytes(const Pyramid& P, int o) {
+  static const int on = [] { const char* e = std::getenv("SIFT_GAUSS_LDS"); return e ? std::atoi(e) : 0; }();
+  if (!on || o == 0 || gauss_vsplit(P, o) || gauss_keep_l64(P, o) || P.oct[o].w < 2) return 0;
+  const int R = P.oct[o].rmax, tw = tile_w(P, o);
+  if (tw + 2 * R > lds_region_stride(tw)) return 0;
+  const size_t b = sizeof(double) * ((size_t)kLY * strip_stride(P, o) + (size_t)(kLY + 2 * R) * lds_region_stride(tw));
+  return b <= 160 * 1024 ? b : 0;
 }
 
 hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st) {
@@ -1306,6 +1619,39 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
   static_assert(kGY == kGaussTileRows, "tile rows");
   const Octave& oc = P.oct[L.o];
   if (L.fuse && !gauss_can_fuse(P, L.o)) return hipErrorInvalidValue;
+  if (const size_t lb = ty_end < 0 && !L.fuse ? lds_path_bytes(P, L.o) : 0) {
+    static bool lattr = false;
+    if (!lattr) {
+      (void)hipFuncSetAttribute((const void*)k_gauss_lds<96, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_gauss_lds<kGX, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      lattr = true;
+    }
+    const int tw = tile_w(P, L.o);
+    L.gx = (oc.w + tw - 1) / tw;
+    L.gy = (oc.h + kLY - 1) / kLY;
+    L.by0 = 0;
+    // one block per CU: split the scales only while the tiles leave CUs idle
+    int G = 1;
+    while (G < P.NS && (long long)L.gx * L.gy * G < 256) ++G;
+    split_scales(P, L.o, G, L.gb);
+    L.G = G;
+    static const int xband = [] { const char* e = std::getenv("SIFT_XCD_BAND"); return e ? std::atoi(e) : -1; }();
+    L.xcd_band = (xband >> (L.o - 1)) & 1;
+    L.sw = strip_stride(P, L.o);
+    static const int dbg = [] { const char* e = std::getenv("SIFT_GAUSS_DBG"); return e ? std::atoi(e) : 0; }();
+    L.dbg = dbg;
+    const bool a16 = !((reinterpret_cast<uintptr_t>(L.dog)) & 15) &&
+                     (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
+    L.vec = (a16 && (oc.w & 3) == 0 && 4.0 * oc.h * oc.w < 2147483648.0) ? 1 : 0;
+    L.zero = oc.rmax > kUR1 ? 1 : 0;
+    if (!L.base) return hipErrorInvalidValue;
+    const dim3 grid(L.gx * L.gy * L.G);
+    if (tw == 96) hipLaunchKernelGGL((k_gauss_lds<96, kUR1>), grid, dim3(512), lb, st, P, L);
+    else hipLaunchKernelGGL((k_gauss_lds<kGX, kUR1>), grid, dim3(512), lb, st, P, L);
+    return hipGetLastError();
+  }
   const int G = scale_groups(P, L.o);
   split_scales(P, L.o, G, L.gb);
   const int tw = tile_w(P, L.o);

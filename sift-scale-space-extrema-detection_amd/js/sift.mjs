@@ -282,9 +282,13 @@ export function findCandidateKeypoints(args, octave_base_images, scales_per_octa
   if (!a || a.differenceOfGaussians === undefined) {
     a = { differenceOfGaussians: args, octaveBaseImages: octave_base_images, scalesPerOctave: scales_per_octave };
   }
-  const { differenceOfGaussians, scalesPerOctave, device = 0 } = a;  // octaveBaseImages: unused (background.js:361)
+  // octaveBaseImages: unused (background.js:361).  withLowContrast: also
+  // return SIFT_findExtremas' lowContrastKeypoints (an extra bitmap, scan and
+  // host copy; the worker's preview stream asks for it, the keypoint path
+  // does not).
+  const { differenceOfGaussians, scalesPerOctave, device = 0, withLowContrast = false } = a;
   const st = ensureDog(differenceOfGaussians, scalesPerOctave, device);
-  const r = native.findExtrema(st.ctx, true);
+  const r = native.findExtrema(st.ctx, !!withLowContrast);
   const O = differenceOfGaussians.length;
   const S = differenceOfGaussians[0].length - 2;
   const group = (ints, values) => {  // [octave][scale-1] = {scaleLevel, localExtremas: [{x, y, value}]}
@@ -304,7 +308,9 @@ export function findCandidateKeypoints(args, octave_base_images, scales_per_octa
   Object.defineProperty(out, 'lowContrastCount', { value: r.lowContrast, enumerable: false });
   // SIFT_findExtremas' lowContrastKeypoints (sift.js:293-306), same shape; the
   // reference does not return them, it posts one marker each (background.js:408-413)
-  Object.defineProperty(out, 'lowContrastKeypoints', { value: group(r.lowInts, r.lowValues), enumerable: false });
+  if (withLowContrast) {
+    Object.defineProperty(out, 'lowContrastKeypoints', { value: group(r.lowInts, r.lowValues), enumerable: false });
+  }
   return attach(out, st, st.gen, { n: r.values.length });
 }
 
@@ -511,7 +517,7 @@ export function createWorkerHandler(post, { matrix2d = true, device = 0, preview
         break;
       }
       case WorkerMessageTypes.FIND_CANDIDATE_KEYPOINTS: {
-        const candidateKeypoints = findCandidateKeypoints({ ...m, device });
+        const candidateKeypoints = findCandidateKeypoints({ ...m, device, withLowContrast: previews });
         if (previews) {  // background.js:380-429
           const dogs = m.differenceOfGaussians;
           const low = candidateKeypoints.lowContrastKeypoints;

@@ -122,7 +122,11 @@ class PipelinedKeypointGather:
             self._settle(slot)
 
     def gathered(self, back=1):
-        """Host view of the step `back` steps ago (1 = the last), rank order."""
+        """Host view of the step `back` steps ago (1 = the last), rank order.
+        Only the last min(steps run, depth) steps are held: an older step's
+        slot has been reused."""
+        if not 1 <= back <= min(self.k, self.depth):
+            raise ValueError("gathered(back=%d): only the last %d step(s) are held" % (back, min(self.k, self.depth)))
         slot = self.slots[(self.k - back) % self.depth]
         self._settle(slot)
         counts, cap = slot["counts"], slot["cap"]

@@ -42,6 +42,15 @@ if (mode !== 'schedule-only') {
   let n2 = 0;
   c2.forEach(oct => oct.forEach(sc => { n2 += sc.localExtremas.length; }));
   out.foreignCandidates = n2;
+  // the low-contrast list only on request, with the count the scan always reports
+  const c3 = sift.findCandidateKeypoints({ differenceOfGaussians: dog, scalesPerOctave: P.scales_per_octave,
+    withLowContrast: true });
+  let nLow = 0;
+  c3.lowContrastKeypoints.forEach(oct => oct.forEach(sc => { nLow += sc.localExtremas.length; }));
+  out.lowListedByDefault = cands.lowContrastKeypoints !== undefined;
+  out.lowContrastListed = nLow;
+  out.lowContrastCount = c3.lowContrastCount;
+  out.lowContrastCountDefault = cands.lowContrastCount;
   // one-call path and its async twin
   out.detect = sift.detect(image, { number_of_octaves: P.num_octaves, scales_per_octave: P.scales_per_octave,
     min_blur_level: P.min_blur, assumed_blur: P.assumed_blur }).length;

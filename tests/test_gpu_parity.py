@@ -481,3 +481,43 @@ def test_loaded_dog_after_range_detection_scans_every_octave(gpu_ctx):
     assert set(np.unique(cref["octave"]).tolist()) >= {0, 1}
     np.testing.assert_array_equal(cand, cref)
     assert low == lref
+
+
+@pytest.mark.timeout(300)
+def test_bench_octave0_schedule_4k_matches_sync():
+    """bench.py's timed schedule at its own configuration (3840x2160, O=4,
+    S=5): three contexts with their own streams, image i+1 ordered after
+    image i's octave-0 pass (sift_order_after AFTER_OCTAVE0), image i settled
+    only after image i+2 is enqueued.  Two different inputs alternate, so a
+    context that mixed up another's planes or lists would show: every image's
+    keypoint records equal a synchronous detection of its input."""
+    W, H = 3840, 2160
+    p = sift_amd.make_params(4, 5)
+    imgs = [np.ascontiguousarray(blob_image(W, H, seed=s), dtype=np.float32) for s in (42, 43)]
+    bufs = [_device_copy(im) for im in imgs]
+    try:
+        ref = []
+        with sift_amd.Context(0) as c:
+            for hip, d in bufs:
+                c.detect_device(d.value, W, H, p)
+                ref.append(c.keypoints().tobytes())
+        assert ref[0] != ref[1]
+        ctxs = [sift_amd.Context(0) for _ in range(3)]
+        try:
+            n_img = 8
+            for i in range(n_img + 2):
+                if i < n_img:
+                    c = ctxs[i % 3]
+                    if i > 0:
+                        c.order_after(ctxs[(i - 1) % 3], sift_amd.AFTER_OCTAVE0)
+                    c.detect_device_async(bufs[i % 2][1].value, W, H, p)
+                j = i - 2
+                if j >= 0:
+                    ctxs[j % 3].detect_wait()
+                    assert ctxs[j % 3].keypoints().tobytes() == ref[j % 2], "image %d" % j
+        finally:
+            for c in ctxs:
+                c.close()
+    finally:
+        for hip, d in bufs:
+            hip.hipFree(d)

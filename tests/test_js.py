@@ -73,6 +73,10 @@ def test_js_stage_chain_matches_reference(name):
     assert np.array_equal(k[:, :4], g.refined[:, :4])
     np.testing.assert_allclose(k[:, 4:7], g.refined[:, 4:7], rtol=0, atol=1e-4)
     assert out["foreignCandidates"] == ref.shape[0]
+    # lowContrastKeypoints only with withLowContrast; the count always
+    assert not out["lowListedByDefault"]
+    assert out["lowContrastListed"] == out["lowContrastCount"] == out["lowContrastCountDefault"]
+    assert out["lowContrastCount"] == int(g.z["low_contrast_counts"].sum())
     assert out["detect"] == g.refined.shape[0]
     assert out["detectAsync"] == [g.refined.shape[0]] * 2  # serialised on the one context
     assert out["busyCode"] == "SIFT_E_BUSY"
