@@ -53,7 +53,6 @@ enum DogSource { kNone = 0, kNative = 1, kForeign = 2 };
 // the kept keypoints per (octave, scale) block from kBlk on.
 constexpr int kBlk = 64;
 constexpr int kCntAll = kBlk + kBlkWords;  // per-block counts, block starts, order flag (sift_kernels.h)
-constexpr int kMaxBands = 16;              // row bands per octave of a banded Gaussian pass
 
 }  // namespace
 
@@ -61,10 +60,6 @@ struct sift_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = true;          // false: the stream of another context (sift_ctx_create_shared)
-  hipStream_t side = nullptr;      // extrema scans of finished octaves, overlapping later octaves' Gaussians
-  hipStream_t hi = nullptr;        // high-priority stream for octave 0's Gaussian+DoG (SIFT_OCT0_PRIO=1)
-  hipEvent_t ev_hi_fork = nullptr, ev_hi_join = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_oct[kMaxOctaves]{};
   std::string err;
   sift_params p{};
   int W = 0, H = 0;
@@ -86,7 +81,6 @@ struct sift_ctx {
   bool ext_pending = false; // extrema launched, counts not yet read back
   bool has_keep = false;    // slots carry keep flags
   bool slots_rows = false;  // slots are the extrema stage's emission (row offsets in rowoff): band order applies
-  bool scans_done = false;  // build_common already launched the extrema scans (side stream)
   bool counters_zeroed = false;  // extrema_prepare zeroed the refinement counters too
   bool detect_pending = false;   // sift_detect_device_async enqueued, sift_detect_wait not yet called
   bool begin_pending = false;    // sift_detect_begin_async enqueued, sift_detect_end_async not yet called
@@ -126,12 +120,6 @@ struct sift_ctx {
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
   hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
-  // Banded pass (octave_bands): octave o >= 1 runs on ost[o], band j of octave
-  // o signals ev_band[o][j]; ev_bfork starts the band streams after the setup.
-  hipStream_t ost[kMaxOctaves]{};
-  hipEvent_t ev_band[kMaxOctaves][kMaxBands]{};
-  hipEvent_t ev_bfork = nullptr;
-  int bands_used = 0;              // bands per octave of the last build (1 = one launch per octave)
   sift_timings tm{};
   std::vector<double> oct_ms;      // per-octave Gaussian+DoG launch time of the last build
 };
@@ -229,30 +217,6 @@ static int ctx_create(int device, sift_ctx* share, sift_ctx** out) {
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
   for (auto& e : ctx->ev_go) (void)hipEventCreate(&e);
   (void)hipEventCreateWithFlags(&ctx->ev_heavy, hipEventDisableTiming);
-  // Measured on MI355X at 4K: overlapping the memory-bound scans with the
-  // small octaves' Gaussians slows both (shared L2/fabric), so the overlap
-  // is opt-in (SIFT_SIDE_STREAM=1).
-  if (std::getenv("SIFT_SIDE_STREAM") && std::atoi(std::getenv("SIFT_SIDE_STREAM"))) {
-    bool ok = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) == hipSuccess;
-    for (auto& e : ctx->ev_oct) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-    if (!ok) {
-      (void)sift_ctx_destroy(ctx);
-      return SIFT_E_HIP;
-    }
-  }
-  if (std::getenv("SIFT_OCT0_PRIO") && std::atoi(std::getenv("SIFT_OCT0_PRIO"))) {
-    int lo = 0, hi = 0;
-    bool ok = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-              hipStreamCreateWithPriority(&ctx->hi, hipStreamNonBlocking, hi) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->ev_hi_fork, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->ev_hi_join, hipEventDisableTiming) == hipSuccess;
-    if (!ok) {
-      (void)sift_ctx_destroy(ctx);
-      return SIFT_E_HIP;
-    }
-  }
   *out = ctx;
   return SIFT_OK;
 }
@@ -268,7 +232,6 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   if (!ctx) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->l64, &ctx->vsplit, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
@@ -283,21 +246,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   for (auto& e : ctx->ev_go)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_heavy) (void)hipEventDestroy(ctx->ev_heavy);
-  for (auto& st : ctx->ost)
-    if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st);
-  for (auto& row : ctx->ev_band)
-    for (auto& e : row)
-      if (e) (void)hipEventDestroy(e);
-  if (ctx->ev_bfork) (void)hipEventDestroy(ctx->ev_bfork);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
-  for (auto& e : ctx->ev_oct)
-    if (e) (void)hipEventDestroy(e);
-  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  if (ctx->side) (void)hipStreamDestroy(ctx->side);
-  if (ctx->hi) (void)hipStreamSynchronize(ctx->hi), (void)hipStreamDestroy(ctx->hi);
-  if (ctx->ev_hi_fork) (void)hipEventDestroy(ctx->ev_hi_fork);
-  if (ctx->ev_hi_join) (void)hipEventDestroy(ctx->ev_hi_join);
   if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SIFT_OK;
@@ -421,55 +370,16 @@ static int extrema_scan(sift_ctx* ctx, int o0, int o1, hipStream_t st);
 // Fused extrema decisions (k_gauss_dog, XF): SIFT_F_FUSED_EXTREMA, or
 // SIFT_FUSE=1 for every detection (experiments).
 static bool fuse_enabled(const sift_params* p) {
-  static const bool env = [] { const char* e = std::getenv("SIFT_FUSE"); return e && std::atoi(e) != 0; }();
+  static const bool env = exp_knob("SIFT_FUSE", 0) != 0;
   return env || (p->flags & SIFT_F_FUSED_EXTREMA);
 }
 
-// Banded Gaussian pass.  Octave 0 is bound by its HBM stores, the small
-// octaves by fp64 issue and load addressing; one launch per octave runs them
-// one after the other.  With bands, octave 0 is launched as SIFT_OBANDS row
-// bands on the context stream and every following octave (up to the first
-// split-pass octave) as bands on a stream of its own, each band waiting only
-// for the bands of the previous octave its seed rows come from (its rows
-// plus the vertical radius), so the small octaves run beside octave 0's
-// stores instead of after them.  The planes are the same bit for bit (every
-// tile runs the same code; only the launch a tile belongs to changes).
-static int octave_bands() {
-  static const int nb = [] {
-    const char* e = std::getenv("SIFT_OBANDS");
-    const int v = e ? std::atoi(e) : 1;
-    return std::max(1, std::min(v, kMaxBands));
-  }();
-  return nb;
-}
-
-static int ensure_band_streams(sift_ctx* ctx, int n_oct) {
-  if (!ctx->ev_bfork) HIPCHK(hipEventCreateWithFlags(&ctx->ev_bfork, hipEventDisableTiming));
-  for (int o = 0; o < n_oct; ++o) {
-    if (o >= 1 && !ctx->ost[o]) HIPCHK(hipStreamCreateWithFlags(&ctx->ost[o], hipStreamNonBlocking));
-    for (auto& e : ctx->ev_band[o])
-      if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
-  return SIFT_OK;
-}
-
-// Band j of nb over t tile rows: [j t / nb, (j + 1) t / nb).
-static int band_begin(int j, int t, int nb) { return (int)((long long)j * t / nb); }
-static int band_of(int row, int t, int nb) {
-  int j = 0;
-  while (j + 1 < nb && band_begin(j + 1, t, nb) <= row) ++j;
-  return j;
-}
-
-// overlap_extrema: launch each octave's extrema scan on the side stream as
-// soon as its DoG planes exist, overlapping the next octaves' Gaussian
-// kernels (memory-bound scans beside FMA-bound small octaves).
 // o_first > 0 (sift_detect_from_seed): no image; the fp64 base of octave
 // o_first is seed_host / seed_dev and octaves o_first .. O-1 are built.
 // fuse_extrema: a detection -- octave 0's extrema decisions run inside its
 // Gaussian+DoG launch (the extrema stage then scans octaves >= 1 only).
 static int build_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
-                        size_t stride, const sift_params* p, const double* sig, bool overlap_extrema = false,
+                        size_t stride, const sift_params* p, const double* sig,
                         int o_first = 0, const double* seed_host = nullptr, const double* seed_dev = nullptr,
                         bool fuse_extrema = false) {
   if (!ctx) return SIFT_E_ARG;
@@ -531,10 +441,8 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     HIPCHK(launch_upsample_base(P, ctx->base0.as<double>(), ctx->stream));
     base0 = ctx->base0.as<double>();
   }
-  ctx->scans_done = false;
   ctx->x_prepared = false;
-  const bool overlap = overlap_extrema && ctx->side;
-  const int nf = (fuse_extrema && !overlap && o_first == 0 && fuse_enabled(p) && gauss_can_fuse(P, 0) &&
+  const int nf = (fuse_extrema && o_first == 0 && fuse_enabled(p) && gauss_can_fuse(P, 0) &&
                   !(p->flags & SIFT_F_LOW_CONTRAST_LIST)) ? 1 : 0;
   if (nf) {  // bitmap geometry, counter resets: before the fused launch writes them
     ctx->dog_source = kNative;
@@ -542,32 +450,11 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     if (rc) return rc;
     ctx->x_prepared = true;
   }
-  if (overlap) {  // the side stream starts after this image's setup, resets the extrema counters
-    ctx->dog_source = kNative;
-    HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
-    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-    rc = extrema_prepare(ctx, ctx->side);
-    if (rc) return rc;
-  }
   const bool xseed = (p->flags & SIFT_F_EXPORT_NEXT_SEED) != 0;
   if (xseed) {
     ctx->xseed_h = (P.oct[P.O - 1].h + 1) / 2;  // background.js:118
     ctx->xseed_w = (P.oct[P.O - 1].w + 1) / 2;
     HIPCHK(ctx->xseed.ensure((size_t)ctx->xseed_h * ctx->xseed_w * sizeof(double)));
-  }
-  // Banded pass: octaves o_first .. ob-1 in row bands (octave_bands above).
-  int nbands = octave_bands(), ob = o_first;
-  if (nbands > 1 && o_first == 0 && !nf && !overlap && !ctx->hi) {
-    while (ob < P.O && !gauss_vsplit(P, ob)) ++ob;
-    if (ob - o_first < 2) ob = o_first;
-  }
-  if (ob == o_first) nbands = 1;
-  ctx->bands_used = nbands;
-  if (nbands > 1) {
-    rc = ensure_band_streams(ctx, ob);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(ctx->ev_bfork, ctx->stream));
-    for (int o = o_first + 1; o < ob; ++o) HIPCHK(hipStreamWaitEvent(ctx->ost[o], ctx->ev_bfork, 0));
   }
   for (int o = o_first; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
@@ -591,63 +478,13 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
       L.X.c_lo = XL.c_lo;
       L.X.c_hi = XL.c_hi;
     }
-    hipStream_t ls = ctx->stream;
-    if (o == 0 && ctx->hi) {  // octave 0 on the high-priority stream, joined back
-      HIPCHK(hipEventRecord(ctx->ev_hi_fork, ctx->stream));
-      HIPCHK(hipStreamWaitEvent(ctx->hi, ctx->ev_hi_fork, 0));
-      ls = ctx->hi;
-    }
     L.l64 = P.oct[o].l64_off >= 0 ? ctx->l64.as<double>() + P.oct[o].l64_off : nullptr;
     L.vsplit = gauss_vsplit(P, o) ? ctx->vsplit.as<double>() : nullptr;
-    if (nbands > 1) {
-      // octaves past the banded ones follow the last banded octave on its stream
-      if (o > o_first) ls = ctx->ost[std::min(o, ob - 1)];
-      if (o < ob) {
-        const int t = gauss_tile_rows(P, o);
-        int waited = -1;
-        for (int j = 0; j < nbands; ++j) {
-          const int t0 = band_begin(j, t, nbands), t1 = band_begin(j + 1, t, nbands);
-          if (o > o_first) {  // the previous octave's bands holding this band's seed rows
-            const int ylast = std::min(oc.h, kGaussTileRows * t1) - 1;
-            const int qmax = std::min(oc.h - 1, ylast + oc.rmax + 8);
-            const int tp = gauss_tile_rows(P, o - 1);
-            const int need = band_of(std::min(tp - 1, 2 * qmax / kGaussTileRows), tp, nbands);
-            for (int b = waited + 1; b <= need; ++b) HIPCHK(hipStreamWaitEvent(ls, ctx->ev_band[o - 1][b], 0));
-            waited = std::max(waited, need);
-          }
-          if (t1 > t0) HIPCHK(launch_gauss_dog(P, L, ls, t0, t1));
-          HIPCHK(hipEventRecord(ctx->ev_band[o][j], ls));
-        }
-      } else {
-        HIPCHK(launch_gauss_dog(P, L, ls));
-      }
-    } else {
-      HIPCHK(launch_gauss_dog(P, L, ls));
-    }
-    if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ls));
-    HIPCHK(hipEventRecord(ctx->ev_go[o], ls));
-    if (ls != ctx->stream && ls == ctx->hi) {
-      HIPCHK(hipEventRecord(ctx->ev_hi_join, ls));
-      HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_hi_join, 0));
-    }
-    if (overlap) {
-      HIPCHK(hipEventRecord(ctx->ev_oct[o], ctx->stream));
-      HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_oct[o], 0));
-      rc = extrema_scan(ctx, o, o + 1, ctx->side);
-      if (rc) return rc;
-    }
-  }
-  if (nbands > 1) {  // the band streams join the context stream
-    for (int o = o_first + 1; o < ob; ++o) HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_go[o], 0));
-    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_go[P.O - 1], 0));
+    HIPCHK(launch_gauss_dog(P, L, ctx->stream));
+    if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_go[o], ctx->stream));
   }
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-  if (overlap) {
-    HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));  // extrema_ms: what the overlap did not hide
-    HIPCHK(hipEventRecord(ctx->ev_join, ctx->side));
-    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
-    ctx->scans_done = true;
-  }
   ctx->dog_source = kNative;
   ctx->have_gauss = keep_gauss;
   ctx->have_cand = false;
@@ -811,8 +648,7 @@ constexpr int kRetry = 1;  // internal: a capacity overflowed, grow and run agai
 
 // The extrema stage, launched without waiting, in three parts:
 //   extrema_prepare  capacities, buffers, counter resets (on stream st);
-//   extrema_scan     bitmap scan of octaves [o0, o1) (k_extrema) on st --
-//                    detect overlaps it with the later octaves' Gaussians;
+//   extrema_scan     bitmap scan of octaves [o0, o1) (k_extrema) on st;
 //   extrema_finish   row-count scan, ordered emission into cand_cap slots,
 //                    exact tie resolution (context stream).
 // Counts stay on the device.
@@ -931,7 +767,7 @@ static int extrema_finish(sift_ctx* ctx) {
     E.cap = ctx->cand_cap;
     // Deferred values (SIFT_DEFER_VALUES=0: gathered here, experiments): the
     // refinement reads each candidate's plane value from its own patch.
-    static const int defer = [] { const char* e = std::getenv("SIFT_DEFER_VALUES"); return e ? std::atoi(e) : 1; }();
+    static const int defer = exp_knob("SIFT_DEFER_VALUES", 1);
     E.deferred = defer != 0;
     HIPCHK(launch_emit(P, E, ctx->stream));
   }
@@ -975,7 +811,7 @@ static int extrema_finish(sift_ctx* ctx) {
   X.keep = ctx->cand_keep.as<unsigned>();
   X.value = ctx->cand_val.as<double>();
   X.counters = cnt;
-  static const int xpos = [] { const char* e = std::getenv("SIFT_XPOS"); return e ? std::atoi(e) : 1; }();
+  static const int xpos = exp_knob("SIFT_XPOS", 1);
   if (xpos) {  // list positions from the emission geometry instead of a binary search
     X.bitmap = ctx->bitmap.as<unsigned long long>();
     X.rowoff = ctx->rowoff.as<unsigned>();
@@ -1086,7 +922,7 @@ static int refine_enqueue(sift_ctx* ctx) {
     R.uncertain = ctx->uncertain.as<unsigned>();
     R.counters = cnt;
     R.perm = nullptr;
-    static const int band_order = [] { const char* e = std::getenv("SIFT_BAND_ORDER"); return e ? std::atoi(e) : 1; }();
+    static const int band_order = exp_knob("SIFT_BAND_ORDER", 1);
     if (band_order && ctx->slots_rows) {
       BandOrder B{};
       B.n_oct = P.O;
@@ -1168,7 +1004,7 @@ static int refine_settle(sift_ctx* ctx) {
   ctx->blk_counts.assign((size_t)ctx->P.O * ctx->P.S, 0);
   if (cap > 0)
     for (size_t b = 0; b < ctx->blk_counts.size(); ++b) ctx->blk_counts[b] = h[kBlk + b];
-  if (std::getenv("SIFT_DEBUG_REFINE"))
+  if (exp_knob("SIFT_DEBUG_REFINE", 0))
     std::fprintf(stderr,
                  "refine uncertain %u: det %u alpha %u omega %u edge_dt %u edge_int %u round %u | iter %u %u %u %u %u"
                  " | output precision %u\n",
@@ -1363,7 +1199,7 @@ int sift_refine(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out, si
 static int detect_begin(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H, size_t stride,
                         const sift_params* p) {
   if (!ctx) return SIFT_E_ARG;
-  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, true, 0, nullptr, nullptr, true);
+  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, 0, nullptr, nullptr, true);
   if (rc) return rc;
   ctx->begin_pending = true;
   ctx->detect_host_img = img_host != nullptr;
@@ -1373,13 +1209,7 @@ static int detect_begin(sift_ctx* ctx, const float* img_host, const float* img_d
 static int detect_end(sift_ctx* ctx) {
   if (!ctx->begin_pending) return set_err(ctx, SIFT_E_STATE, "no detection begun (sift_detect_begin_async)");
   ctx->begin_pending = false;
-  int rc;
-  if (ctx->scans_done) {
-    ctx->scans_done = false;
-    rc = extrema_finish(ctx);
-  } else {
-    rc = launch_extrema_stage(ctx);
-  }
+  int rc = launch_extrema_stage(ctx);
   if (rc) return rc;
   rc = refine_enqueue(ctx);
   if (rc) return rc;
@@ -1546,7 +1376,7 @@ static int detect_from_seed(sift_ctx* ctx, int o_first, const double* seed_host,
   if (o_first < 1) return set_err(ctx, SIFT_E_ARG, "octave_first must be >= 1");
   if (scan_first && (scan_first < o_first || scan_first >= p->num_octaves))
     return set_err(ctx, SIFT_E_ARG, "octave_scan_first outside [octave_first, num_octaves)");
-  int rc = build_common(ctx, nullptr, nullptr, W, H, 0, p, nullptr, false, o_first, seed_host, seed_dev);
+  int rc = build_common(ctx, nullptr, nullptr, W, H, 0, p, nullptr, o_first, seed_host, seed_dev);
   if (rc) return rc;
   if (scan_first) ctx->scan_first = scan_first;
   rc = launch_extrema_stage(ctx);

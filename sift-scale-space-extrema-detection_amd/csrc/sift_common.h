@@ -10,8 +10,23 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 namespace sift {
+
+// Experiment knobs: with -DSIFT_EXPERIMENTS (tools/build_variant.sh A/B
+// builds) the named environment variable overrides the default; the shipping
+// library (`make lib`) reads no environment and always takes the default,
+// the measured winner.
+inline int exp_knob(const char* name, int dflt) {
+#ifdef SIFT_EXPERIMENTS
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
 
 constexpr int kMaxOctaves = 12;
 constexpr int kMaxScales = 12;   // S+3 <= kMaxScales  (S <= 9)

@@ -363,12 +363,11 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
   // scan's blocks per CU (160 KiB / SIFT_XLDS) to leave CUs to other images.
   // Values outside [0, 160 KiB] are ignored.
   static const int xlds = [] {
-    const char* e = std::getenv("SIFT_XLDS");
-    const long v = e ? std::strtol(e, nullptr, 10) : 0;
-    return (v > 0 && v <= 160 * 1024) ? (int)v : 0;
+    const int v = exp_knob("SIFT_XLDS", 0);
+    return (v > 0 && v <= 160 * 1024) ? v : 0;
   }();
   // SIFT_XXCD=0: plain round-robin block order (experiments)
-  static const int xxcd = [] { const char* e = std::getenv("SIFT_XXCD"); return e ? std::atoi(e) : 1; }();
+  static const int xxcd = exp_knob("SIFT_XXCD", 1);
   L.xcd_band = xxcd != 0;
   const void* fn = L.lowbitmap ? (const void*)k_extrema<true> : (const void*)k_extrema<false>;
   if (xlds > 65536) {
@@ -397,12 +396,12 @@ size_t exact_lds_bytes(const Pyramid& P) {
 
 hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, hipStream_t st) {
   const unsigned grid = std::max(1u, std::min(X.amb_cap, 4096u));
-  static const bool attr = [] {  // scratch of radii above ~335 exceeds 64 KiB
-    (void)hipFuncSetAttribute((const void*)k_exact_extrema, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return true;
-  }();
-  (void)attr;
-  hipLaunchKernelGGL(k_exact_extrema, dim3(grid), dim3(64), exact_lds_bytes(P), st, P, X);
+  const size_t lds = exact_lds_bytes(P);
+  if (lds > 64 * 1024) {  // scratch of radii above ~335
+    const hipError_t e = hipFuncSetAttribute((const void*)k_exact_extrema, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_exact_extrema, dim3(grid), dim3(64), lds, st, P, X);
   return hipGetLastError();
 }
 

@@ -1169,6 +1169,215 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
 }
 
 // ---------------------------------------------------------------------------
+// Producer / consumer waves (octaves >= 1).  In k_gauss_dog every wave runs
+// its scale loop as vertical pass (base loads: TA / L2 bound) -> horizontal
+// pass -> plane stores (LDS / HBM-store bound), and the waves of a CU move
+// through these phases together, so the phases add up instead of
+// overlapping; each scale's first base load also waits behind the previous
+// scale's stores (vmcnt counts both, in issue order).  Here a block has 8
+// waves for a TW x 32 tile: waves 0-3 (producers) run the vertical passes
+// of rows 8 w .. 8 w + 7 into one of two strips, waves 4-7 (consumers) run
+// the horizontal passes and the epilogue of the same rows from the other
+// strip, one scale behind:
+//
+//   producers  V(s0) | V(s0+1) | V(s0+2) | ...
+//   consumers        | H(s0)   | H(s0+1) | ...     (one LDS barrier per scale)
+//
+// so every CU always has load-bound and store-bound work in flight, and the
+// producers never store (their loads wait for nothing else) nor the
+// consumers load from global memory.  Same strips, same fma chains per
+// output as k_gauss_dog (bit-identical planes).
+// ---------------------------------------------------------------------------
+template <int TW, int RMAX>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_gauss_ws(const Pyramid P,
+                                                                                      const GaussLaunch L) {
+  constexpr int NI = TW == kGX ? kNR : 3;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Octave& oc = P.oct[L.o];
+  int lb = blockIdx.x;
+  if (L.xcd_band) {
+    const int nb = L.gx * L.gy * L.G, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    lb = xc * q + min(xc, rm) + (lb >> 3);
+  }
+  const int bz = lb % L.G, bt = lb / L.G;
+  const int bx = bt % L.gx, by = bt / L.gx;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool producer = wave < 4;
+  GTile T;
+  T.bx = bx;
+  T.h = oc.h;
+  T.w = oc.w;
+  T.x0 = bx * TW;
+  T.y0 = by * kGY;
+  T.lane = threadIdx.x & 63;
+  T.wv = wave & 3;  // slab: rows 8 wv .. 8 wv + 7 of the tile
+  T.cg = T.lane & (kCG - 1);
+  T.rs = T.lane / kCG;
+  if constexpr (TW == 96) {
+    int g, j;  // conflict-free ds_read_b128 item map
+    b128_group(T.lane, g, j);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      T.icg[i] = 8 * i + (j & 7);
+      T.irow[i] = 2 * g + (j >> 3);
+    }
+  }
+  auto irw = [&](int i) { return TW == kGX ? T.rs + kRS * i : T.irow[i]; };
+  auto icg = [&](int i) { return TW == kGX ? T.cg : T.icg[i]; };
+  T.sw = L.sw;
+  T.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L.base), 0, T.h * T.w * 8, 0x00020000);
+  const int nstrip = kGY * T.sw;
+  if (L.zero)
+    for (int i = threadIdx.x; i < 2 * nstrip; i += 512) smem[i] = 0.0;
+  const long long plane = (long long)T.h * T.w;
+  const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
+  const int s_first = max(0, s_begin - 1);
+  __syncthreads();  // zeroed strips
+
+  const bool st = !(L.dbg & 1);
+  int voff[NI];
+  bool own[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int y = T.y0 + 8 * T.wv + irw(i);
+    const int x = T.x0 + 4 * icg(i);
+    own[i] = y < T.h && T.w - x > 0;
+    voff[i] = own[i] ? (y * T.w + x) * 4 : 0x7ffffff0;
+  }
+  // Separate loops (the same number of barriers on both sides): no value of
+  // one role is live in the other's code.
+  if (producer) {  // scale s into strip s & 1, one scale ahead of the consumers
+    for (int s = s_first; s < s_end; ++s) {
+      double* V = smem + (s & 1) * nstrip;
+      GTile Ts = T;
+      asm volatile("" : "+v"(Ts.lane));
+      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+      if (L.vsplit) vert_copy(Ts, oc.rad[s], L.vsplit + (long long)s * plane, V);
+      else if constexpr (TW == 96) vert96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V);
+      else vert_any<false, RMAX>(Ts, oc.rad[s], wp, V);
+      lds_barrier();  // strip s written; strip s - 1 read by the consumers
+    }
+    lds_barrier();
+    return;
+  }
+  lds_barrier();  // the producers' first strip
+  double lprev[NI][4];
+  const int nS = P.S;
+  for (int s = s_first; s < s_end; ++s) {
+    if constexpr (TW == 96) {
+      // items 0-1 side by side, then 2, each group with its epilogue (only
+      // one group's chains and reads live: k_gauss_dog's SIFT_TW96_SEQ 2)
+      const double* V = smem + (s & 1) * nstrip;
+      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+      GTile Ts = T;
+      asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
+      const unsigned pb = (unsigned)plane * 4u;
+      const bool stor = s >= s_begin && st;
+      const __amdgpu_buffer_rsrc_t rg =
+          __builtin_amdgcn_make_buffer_rsrc(L.gauss ? L.gauss + s * plane : L.dog, 0, pb, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rd =
+          __builtin_amdgcn_make_buffer_rsrc(L.dog + (s > 0 ? s - 1 : 0) * plane, 0, pb, 0x00020000);
+      horz96s_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V,
+                   [&](int i, const double (&o)[4]) {
+                     double d[4];
+#pragma unroll
+                     for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[q];
+                     const int y = T.y0 + 8 * T.wv + irw(i);
+                     const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
+                     if (stor) {
+                       if (L.vec) {
+                         if (L.gauss) bstore4(rg, voff[i], o);
+                         if (s > 0) bstore4(rd, voff[i], d);
+                       } else if (own[i]) {
+                         const long long pp = (long long)y * T.w + x;
+                         if (L.gauss) store4(L.gauss + s * plane + pp, o, nvalid);
+                         if (s > 0) store4(L.dog + (s - 1) * plane + pp, d, nvalid);
+                       }
+                     }
+                     if (s == nS && L.next_seed && s >= s_begin && own[i] && !(y & 1)) {
+                       double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+                       sd[0] = o[0];
+                       if (nvalid > 2) sd[1] = o[2];
+                     }
+#pragma unroll
+                     for (int q = 0; q < 4; ++q) lprev[i][q] = o[q];
+                   });
+    } else {
+      const double* V = smem + (s & 1) * nstrip;
+      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+      GTile Ts = T;
+      asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
+      double out[NI][4];
+      if constexpr (TW == 96) horz96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V, out);
+      else horz_any<false, RMAX>(Ts, oc.rad[s], wp, V, out);
+      double d[NI][4];
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
+      if (s >= s_begin && (st || out[0][0] == 12345.0)) {
+        if (L.vec) {
+          const unsigned pb = (unsigned)plane * 4u;
+          if (L.gauss) {
+            const __amdgpu_buffer_rsrc_t rg =
+                __builtin_amdgcn_make_buffer_rsrc(L.gauss + s * plane, 0, pb, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) bstore4(rg, voff[i], out[i]);
+          }
+          if (s > 0) {
+            const __amdgpu_buffer_rsrc_t rd =
+                __builtin_amdgcn_make_buffer_rsrc(L.dog + (s - 1) * plane, 0, pb, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < NI; ++i) bstore4(rd, voff[i], d[i]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
+            const int y = T.y0 + 8 * T.wv + irw(i);
+            const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
+            if (own[i]) {
+              const long long pp = (long long)y * T.w + x;
+              if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
+              if (s > 0) store4(L.dog + (s - 1) * plane + pp, d[i], nvalid);
+            }
+          }
+        }
+      }
+      if (L.l64 && s >= s_begin) {  // fp64 plane for the exact passes
+        double* lp = L.l64 + s * plane;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int y = T.y0 + 8 * T.wv + irw(i);
+          const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
+          if (own[i]) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (q < nvalid) lp[(long long)y * T.w + x + q] = out[i][q];
+          }
+        }
+      }
+      if (s == P.S && L.next_seed && s >= s_begin) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int y = T.y0 + 8 * T.wv + irw(i);
+          const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
+          if (own[i] && !(y & 1)) {
+            double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+            sd[0] = out[i][0];
+            if (nvalid > 2) sd[1] = out[i][2];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
+    }
+    lds_barrier();  // strip s read by the consumers, strip s + 1 written by the producers
+  }
+}
+
+// ---------------------------------------------------------------------------
 // LDS-resident base (octaves >= 1 whose base region and strip fit one CU's
 // LDS: 4K / 8K octaves 1 and 2).  k_gauss_dog's octaves >= 1 re-read the
 // base region from L1/L2 once per SCALE: S+3 passes of 16-byte loads whose
@@ -1462,14 +1671,14 @@ bool gauss_needs_base0(const Pyramid& P) { return P.oct[0].rmax > kUR; }
 // instead of recomputing 3x3x3 patches with 189- and 377-tap chains (8K O=6
 // S=5: octaves 4 and 5; at 4K octave 3, radius 47, it measured slower: 0.71 -> 0.74 ms pass).
 bool gauss_keep_l64(const Pyramid& P, int o) {
-  static const int rmin = [] { const char* e = std::getenv("SIFT_L64_R"); return e ? std::atoi(e) : 90; }();
+  static const int rmin = exp_knob("SIFT_L64_R", 90);
   return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin;
 }
 
 // Octaves o >= 1 whose largest radius reaches SIFT_VSPLIT_R (default 40; 0 =
 // never) run the split vertical pass (k_gauss_vert) before the tile kernel.
 bool gauss_vsplit(const Pyramid& P, int o) {
-  static const int rmin = [] { const char* e = std::getenv("SIFT_VSPLIT_R"); return e ? std::atoi(e) : 40; }();
+  static const int rmin = exp_knob("SIFT_VSPLIT_R", 40);
   return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin;
 }
 
@@ -1478,7 +1687,7 @@ static bool staged0(const Pyramid& P, int o) { return o == 0 && !gauss_needs_bas
 // 96-column tiles (horz_full96) for octaves >= 1 whose radii all have
 // unrolled code and no split pass (SIFT_TW96=0: always 64, experiments).
 static int tile_w(const Pyramid& P, int o) {
-  static const int tw96 = [] { const char* e = std::getenv("SIFT_TW96"); return e ? std::atoi(e) : 1; }();
+  static const int tw96 = exp_knob("SIFT_TW96", 1);
   const Octave& oc = P.oct[o];
   return (tw96 && o >= 1 && kVert2 && oc.rmax <= kUR1 && oc.w >= 2 && !gauss_vsplit(P, o)) ? 96 : kGX;
 }
@@ -1560,12 +1769,14 @@ static int split_scales(const Pyramid& P, int o, int G, int* gb) {
 static int scale_groups(const Pyramid& P, int o) {
   static const std::vector<int> env = [] {
     std::vector<int> v;
+#ifdef SIFT_EXPERIMENTS
     if (const char* e = std::getenv("SIFT_GAUSS_GROUPS"))
       for (const char* p = e; *p;) {
         v.push_back(std::atoi(p));
         while (*p && *p != ',') ++p;
         if (*p) ++p;
       }
+#endif
     return v;
   }();
   if (o == 0) return 1;
@@ -1577,12 +1788,10 @@ static int scale_groups(const Pyramid& P, int o) {
   const Octave& oc = P.oct[o];
   const int tw = tile_w(P, o);
   const long long tiles = (long long)((oc.w + tw - 1) / tw) * ((oc.h + kGY - 1) / kGY);
-  // Split-pass octaves recompute only the horizontal pass of the scale
-  // before a group: split them until ~8 waves per SIMD (their chains are
-  // latency-bound at radius 47+).
-  const long long target = gauss_vsplit(P, o) ? 2048 : 400;
+  // (Split-pass octaves measured the same: 2048 instead of 400 blocks made
+  // 4K octave 3 0.054 -> 0.073 ms.)
   int g = 1;
-  while (g < P.NS && tiles * g < target) ++g;
+  while (g < P.NS && tiles * g < 400) ++g;
   return g;
 }
 
@@ -1598,7 +1807,7 @@ static void set_attr() {
 // columns, or more than the CU's 160 KiB).  SIFT_GAUSS_LDS=0 turns it off
 // (A/B against k_gauss_dog).
 static size_t lds_path_bytes(const Pyramid& P, int o) {
-  static const int on = [] { const char* e = std::getenv("SIFT_GAUSS_LDS"); return e ? std::atoi(e) : 0; }();
+  static const int on = exp_knob("SIFT_GAUSS_LDS", 0);
   if (!on || o == 0 || gauss_vsplit(P, o) || gauss_keep_l64(P, o) || P.oct[o].w < 2) return 0;
   const int R = P.oct[o].rmax, tw = tile_w(P, o);
   if (tw + 2 * R > lds_region_stride(tw)) return 0;
@@ -1637,10 +1846,10 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     while (G < P.NS && (long long)L.gx * L.gy * G < 256) ++G;
     split_scales(P, L.o, G, L.gb);
     L.G = G;
-    static const int xband = [] { const char* e = std::getenv("SIFT_XCD_BAND"); return e ? std::atoi(e) : -1; }();
+    static const int xband = exp_knob("SIFT_XCD_BAND", -1);
     L.xcd_band = (xband >> (L.o - 1)) & 1;
     L.sw = strip_stride(P, L.o);
-    static const int dbg = [] { const char* e = std::getenv("SIFT_GAUSS_DBG"); return e ? std::atoi(e) : 0; }();
+    static const int dbg = exp_knob("SIFT_GAUSS_DBG", 0);
     L.dbg = dbg;
     const bool a16 = !((reinterpret_cast<uintptr_t>(L.dog)) & 15) &&
                      (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
@@ -1668,8 +1877,8 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
   // XCD-banded tile order for octaves >= 1 (SIFT_XCD_BAND: bit o-1 of the
   // value; default all).  Measured (4K, O=4, S=5): isolated pass 0.748 ->
   // 0.730 ms, pipelined bench +0.5-1 % (tools/gpu_envab.sh).
-  static const int xband = [] { const char* e = std::getenv("SIFT_XCD_BAND"); return e ? std::atoi(e) : -1; }();
-  static const int xband0 = [] { const char* e = std::getenv("SIFT_XCD_BAND0"); return e ? std::atoi(e) : 0; }();
+  static const int xband = exp_knob("SIFT_XCD_BAND", -1);
+  static const int xband0 = exp_knob("SIFT_XCD_BAND0", 0);
   L.xcd_band = L.o >= 1 ? ((xband >> (L.o - 1)) & 1) : xband0;
   const dim3 grid(L.gx * L.gy * L.G);
   const size_t lds = gauss_lds_bytes(P, L.o, L.fuse != 0);
@@ -1683,7 +1892,7 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     attr_set = true;
   }
   L.sw = strip_stride(P, L.o);
-  static const int dbg = [] { const char* e = std::getenv("SIFT_GAUSS_DBG"); return e ? std::atoi(e) : 0; }();
+  static const int dbg = exp_knob("SIFT_GAUSS_DBG", 0);
   L.dbg = dbg;
   const bool a16 = !((reinterpret_cast<uintptr_t>(L.dog)) & 15) &&
                    (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
@@ -1693,6 +1902,22 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     if (L.o == 0 || !L.base) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_gauss_vert, dim3((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, P.NS), dim3(256), 0, st, P,
                        L.o, L.base, L.vsplit);
+  }
+  // Producer / consumer waves (k_gauss_ws) for octaves >= 1 whose two
+  // strips fit the CU's LDS (SIFT_GAUSS_WS=0: k_gauss_dog, A/B builds).
+  static const int ws = exp_knob("SIFT_GAUSS_WS", 0);
+  if (ws && L.o >= 1 && !L.fuse && ty_end < 0 && oc.w >= 2 && 2 * lds <= 160 * 1024) {
+    static bool wattr = false;
+    if (!wattr) {
+      (void)hipFuncSetAttribute((const void*)k_gauss_ws<96, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_gauss_ws<kGX, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      wattr = true;
+    }
+    if (tw == 96) hipLaunchKernelGGL((k_gauss_ws<96, kUR1>), grid, dim3(512), 2 * lds, st, P, L);
+    else hipLaunchKernelGGL((k_gauss_ws<kGX, kUR1>), grid, dim3(512), 2 * lds, st, P, L);
+    return hipGetLastError();
   }
   if (L.fuse) {  // staged octave 0 (gauss_can_fuse)
     if (L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, true>), grid, dim3(256), lds, st, P, L);

@@ -627,12 +627,12 @@ hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream
 hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, hipStream_t st) {
   if (R.cap <= 0) return hipSuccess;
   const int grid = std::max(1, std::min(R.cap, 8192));
-  static const bool attr = [] {  // scratch of radii above ~335 exceeds 64 KiB
-    (void)hipFuncSetAttribute((const void*)k_refine_exact, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return true;
-  }();
-  (void)attr;
-  hipLaunchKernelGGL(k_refine_exact, dim3(grid), dim3(64), exact_lds_bytes(P), st, P, R);
+  const size_t lds = exact_lds_bytes(P);
+  if (lds > 64 * 1024) {  // scratch of radii above ~335
+    const hipError_t e = hipFuncSetAttribute((const void*)k_refine_exact, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_refine_exact, dim3(grid), dim3(64), lds, st, P, R);
   return hipGetLastError();
 }
 

@@ -77,7 +77,10 @@ function bump(st, stage, W, H, params) {
 }
 
 function attach(obj, st, gen, extra) {
-  Object.defineProperty(obj, HANDLE, { value: Object.assign({ st, gen }, extra), enumerable: false });
+  // configurable: a stale object (its device pyramid replaced since) is
+  // re-uploaded and re-attached when a later stage is given it again
+  Object.defineProperty(obj, HANDLE, { value: Object.assign({ st, gen }, extra), enumerable: false,
+    configurable: true });
   return obj;
 }
 
