@@ -179,6 +179,10 @@ def main():
     ap.add_argument("--batch", type=int, default=1,
                     help="independent images per GPU per step (BASELINE cfg 4: --width 1920 --height 1080 "
                          "--batch 8 on 8 GPUs = 64 images per step)")
+    ap.add_argument("--batch-mode", default="launch", choices=["launch", "images"],
+                    help="with --batch B > 1: launch = the B images as ONE batched detection per step "
+                         "(sift_detect_batch_device: one launch per stage over the batch), images = B separate "
+                         "detections per step")
     ap.add_argument("--inflight", type=int, default=3,
                     help="detections in flight per GPU (one context each; the host settles image k while "
                          "image k+1 runs)")
@@ -235,6 +239,15 @@ def main():
 
     img = blob_image(W, H, seed=42 + rank)
     d_img = torch.from_numpy(img).to("cuda:%d" % dev)
+    Bt = max(1, args.batch)
+    batched = Bt > 1 and args.batch_mode == "launch"
+    if batched and args.overlap == "phased":
+        print("bench.py: --overlap phased does not apply to batched launches", file=sys.stderr)
+        return 2
+    d_imgs = None
+    if batched:  # B distinct images back to back in HBM (image 0 is the rank's usual image)
+        d_imgs = torch.from_numpy(np.stack([img] + [blob_image(W, H, seed=1000 + 64 * rank + i)
+                                                   for i in range(1, Bt)])).to("cuda:%d" % dev)
     torch.cuda.synchronize(dev)
     nin = max(1, args.inflight)
     ctxs = [sift_amd.Context(dev)]
@@ -276,7 +289,10 @@ def main():
             return
         if after is not None and i > 0 and nin > 1:
             c.order_after(ctxs[(i - 1) % nin], after)
-        c.detect_device_async(d_img.data_ptr(), W, H, params)
+        if batched:
+            c.detect_batch_device_async(d_imgs.data_ptr(), Bt, W, H, params)
+        else:
+            c.detect_device_async(d_img.data_ptr(), W, H, params)
 
     def flush():
         if pend[0] is not None:
@@ -308,7 +324,7 @@ def main():
         c.synchronize()
     t0 = time.perf_counter()
     n_total = 0
-    NI = args.steps * max(1, args.batch)  # images in the timed region
+    NI = args.steps * (1 if batched else Bt)  # detections (images, or batches) in the timed region
     for i in range(NI):  # image i is enqueued before image i-(nin-1) is settled
         launch(i)
         if i >= nin - 1:
@@ -359,9 +375,10 @@ def main():
             e = torch.tensor([ts], dtype=torch.float64, device="cuda:%d" % dev)
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             ts = float(e.item())
-        sustained = {"images_per_gpu": ns, "seconds": round(ts, 3),
-                     "value": round(world * ns * W * H / ts / 1e6, 3), "unit": "Mpix/s",
-                     "ms_per_image": round(ts / ns * 1e3, 4)}
+        ipd = Bt if batched else 1  # images per detection
+        sustained = {"images_per_gpu": ns * ipd, "seconds": round(ts, 3),
+                     "value": round(world * ns * ipd * W * H / ts / 1e6, 3), "unit": "Mpix/s",
+                     "ms_per_image": round(ts / (ns * ipd) * 1e3, 4)}
     # After the timed region: the same detection alone (one image in flight,
     # nothing overlapping), so the kernel's isolated duration is on record
     # beside its pipelined one.
@@ -369,7 +386,10 @@ def main():
     iso_oct = [0.0] * O
     n_iso = 10
     for _ in range(n_iso):
-        ctx.detect_device_async(d_img.data_ptr(), W, H, params)
+        if batched:
+            ctx.detect_batch_device_async(d_imgs.data_ptr(), Bt, W, H, params)
+        else:
+            ctx.detect_device_async(d_img.data_ptr(), W, H, params)
         ctx.detect_wait()
         t = ctx.timings()
         for k in iso:
@@ -377,13 +397,19 @@ def main():
         for o, v in enumerate(ctx.octave_timings()):
             iso_oct[o] += v / n_iso
     with sift_amd.Context(dev) as vctx:
-        vctx.detect_device(d_img.data_ptr(), W, H, params)
-        verified = vctx.keypoints().tobytes() == kp_timed
+        if batched:  # the batch against the same images detected one by one
+            ref = []
+            for b in range(Bt):
+                vctx.detect_device(d_imgs[b].data_ptr(), W, H, params)
+                ref.append(vctx.keypoints().tobytes())
+            verified = b"".join(ref) == kp_timed
+        else:
+            vctx.detect_device(d_img.data_ptr(), W, H, params)
+            verified = vctx.keypoints().tobytes() == kp_timed
     if not verified:
         print("bench.py: rank %d: the timed region's last keypoint list differs from a synchronous detection"
               % rank, file=sys.stderr)
     K = args.steps
-    Bt = max(1, args.batch)
     ms_per_step = elapsed / K * 1e3
     value = world * Bt * W * H / (elapsed / K) / 1e6
     counts = ctxs[(NI - 1) % nin].counts()
@@ -391,8 +417,9 @@ def main():
     if rank == 0:
         gauss_ms = stage["gauss_dog_ms"] / NI
         oct0_ms = stage["gauss_oct0_ms"] / NI
-        B = alg_bytes(W, H, O, S, args.skip_gauss_planes)
-        Bo = octave_bytes(W, H, O, S, args.skip_gauss_planes)
+        ipd = Bt if batched else 1  # the pass of one detection covers ipd images
+        B = ipd * alg_bytes(W, H, O, S, args.skip_gauss_planes)
+        Bo = [ipd * b for b in octave_bytes(W, H, O, S, args.skip_gauss_planes)]
         B0 = Bo[0]
         gbs = lambda b, ms: b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         cfg_key = "%dx%d_o%d_s%d%s" % (W, H, O, S, "_nogauss" if args.skip_gauss_planes else "")
@@ -401,7 +428,7 @@ def main():
         pipelined_note = ("pipelined: %d images in flight on %d streams, each launch's window includes "
                           "waiting for CUs held by the other images' kernels" % (nin, nin)
                           if own and nin > 1 else "one image at a time")
-        B_x = extrema_bytes(W, H, O, S)
+        B_x = ipd * extrema_bytes(W, H, O, S)
         iso_pass = iso["gauss_dog_ms"]
         out = {
             "metric": metric_name(W, H, O, S, Bt),
@@ -423,6 +450,7 @@ def main():
                              ", Gaussian planes not materialised" if args.skip_gauss_planes else ""),
                 "width": W, "height": H, "octaves": O, "scales_per_octave": S,
                 "images_per_gpu": Bt, "global_batch": world * Bt, "inflight_per_gpu": nin,
+                "batch_launch": batched,
                 "streams_per_gpu": nin if own else 1,
                 "overlap": args.overlap,
                 "parallelism": ("dp%d (%d image%s per GPU, RCCL keypoint all-gather)" % (world, Bt, "s" if Bt > 1 else "")
@@ -435,12 +463,17 @@ def main():
             "candidates": counts["candidates"],
             "keypoints_all_ranks": n_total,
             "verified": verified,
-            "verified_what": ("rank 0: the last timed image's keypoint records (pipelined schedule, %d contexts) "
-                              "byte-identical to a synchronous sift_detect_device of the same input on a fresh "
-                              "context" % nin),
+            "verified_what": (("rank 0: the last timed batch's keypoint records (one batched detection of %d "
+                               "distinct images, pipelined schedule, %d contexts) byte-identical to the %d images "
+                               "detected one by one (sift_detect_device) on a fresh context" % (Bt, nin, Bt))
+                              if batched else
+                              ("rank 0: the last timed image's keypoint records (pipelined schedule, %d contexts) "
+                               "byte-identical to a synchronous sift_detect_device of the same input on a fresh "
+                               "context" % nin)),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "Gaussian+DoG pass: k_gauss_dog, %d launches (one per octave)" % O,
+                "kernel": "Gaussian+DoG pass: k_gauss_dog, %d launches (one per octave%s)" %
+                          (O, ", each over the batch of %d images" % Bt if batched else ""),
                 "achieved": round(gbs(B, iso_pass), 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 5
+#define SIFT_ABI_VERSION 6
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -222,6 +222,26 @@ int sift_last_counts(struct sift_ctx *ctx, size_t *n_candidates, size_t *n_low_c
 int sift_detect_device_async(struct sift_ctx *ctx, const float *d_img, int width, int height,
                              size_t stride_px, const sift_params *p);
 int sift_detect_wait(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out);
+
+/* A batch of n_images independent device images of one geometry (ABI
+ * version >= 6; BASELINE cfg 4's images per GPU): image b is width x height
+ * at d_imgs + b * image_stride_px (row stride stride_px).  Each stage is ONE
+ * launch over the whole batch -- a Gaussian+DoG launch per octave, one
+ * extrema scan, one refinement -- with the planes image-major.  Per image the
+ * results are exactly those of sift_detect_device on that image (the
+ * reference's per-image path, background.js:71-685, run once per image); the
+ * keypoints come out image-major, each image's in the reference's order, and
+ * sift_last_block_counts gives n_images * num_octaves * scales_per_octave
+ * block counts (image-major), so image b's count is the sum of its blocks.
+ * Plain detection only: no low-contrast list, fused decisions, crops, owned
+ * rows or exported seeds (SIFT_E_UNSUPPORTED); the candidate list of a batch
+ * is not exposed.  _async enqueues it (sift_detect_wait completes it). */
+int sift_detect_batch_device(struct sift_ctx *ctx, const float *d_imgs, int n_images, size_t image_stride_px,
+                             int width, int height, size_t stride_px, const sift_params *p,
+                             sift_keypoint *out, size_t cap, size_t *n_out);
+int sift_detect_batch_device_async(struct sift_ctx *ctx, const float *d_imgs, int n_images,
+                                   size_t image_stride_px, int width, int height, size_t stride_px,
+                                   const sift_params *p);
 
 /* The same detection in two phases (ABI version >= 4): _begin enqueues the
  * Gaussian+DoG pass, _end the extrema scan and refinement; sift_detect_wait

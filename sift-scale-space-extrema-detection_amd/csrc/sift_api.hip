@@ -102,6 +102,7 @@ struct sift_ctx {
   DBuf base0;                                  // materialised octave-0 base (large radii only)
   DBuf l64;                                    // fp64 Gaussian planes of the large-radius octaves
   DBuf vsplit;                                 // vertical-sum scratch of the split-pass octaves (one at a time)
+  long long vsplit_pi = 0;                     // ... doubles per image of a batch
   std::vector<double> wts_host;                // taps last uploaded to wts
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
@@ -339,6 +340,8 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
     }
   }
   if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");
+  P.nimg = 1;  // one image (build_common sets a batch)
+  P.kpi = (unsigned)koff;
   // LDS feasibility of the Gaussian kernel (two strips of 32 rows x (76 + 2R) fp64).
   for (int o = 0; o < O; ++o)
     if (gauss_lds_bytes(P, o) > 160 * 1024)
@@ -378,10 +381,13 @@ static bool fuse_enabled(const sift_params* p) {
 // o_first is seed_host / seed_dev and octaves o_first .. O-1 are built.
 // fuse_extrema: a detection -- octave 0's extrema decisions run inside its
 // Gaussian+DoG launch (the extrema stage then scans octaves >= 1 only).
+// nimg > 1: a batch of nimg device images of one geometry, image b at
+// img_dev + b * img_bstride (sift_detect_batch_device): one launch per stage
+// over all of them, planes and seeds image-major.
 static int build_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
                         size_t stride, const sift_params* p, const double* sig,
                         int o_first = 0, const double* seed_host = nullptr, const double* seed_dev = nullptr,
-                        bool fuse_extrema = false) {
+                        bool fuse_extrema = false, int nimg = 1, size_t img_bstride = 0) {
   if (!ctx) return SIFT_E_ARG;
   if (o_first == 0 && !img_host && !img_dev) return set_err(ctx, SIFT_E_ARG, "null image");
   if (o_first > 0 && !seed_host && !seed_dev) return set_err(ctx, SIFT_E_ARG, "null seed");
@@ -396,10 +402,22 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   ctx->has_xseed = false;
   const long long tot = total_plane_px(ctx);
   const bool keep_gauss = !(p->flags & SIFT_F_SKIP_GAUSS_PLANES);
-  HIPCHK(ctx->dog.ensure((size_t)tot * P.ND * sizeof(float)));
-  if (keep_gauss) HIPCHK(ctx->gauss.ensure((size_t)tot * P.NS * sizeof(float)));
-  HIPCHK(ctx->seeds.ensure((size_t)std::max<long long>(1, tot - (long long)P.oct[0].h * P.oct[0].w) *
-                           sizeof(double)));
+  if (nimg > 1) {
+    if (o_first != 0 || img_host || !img_dev || fuse_extrema || gauss_needs_base0(P) || ctx->row0 != 0 ||
+        ctx->own_lo >= 0 || (p->flags & (SIFT_F_EXPORT_NEXT_SEED | SIFT_F_LOW_CONTRAST_LIST | SIFT_F_FUSED_EXTREMA)))
+      return set_err(ctx, SIFT_E_UNSUPPORTED, "batch: whole device images, plain detection only");
+    if ((unsigned long long)P.kpi * (unsigned long long)nimg > 0xffffffffull ||
+        (long long)nimg * P.O * P.S > kBlkN)
+      return set_err(ctx, SIFT_E_UNSUPPORTED, "batch too large for 32-bit keys / block counts");
+  }
+  const long long seeds_pi = std::max<long long>(1, tot - (long long)P.oct[0].h * P.oct[0].w);
+  P.nimg = nimg;
+  P.img_bstride = nimg > 1 ? (long long)img_bstride : 0;
+  P.seed_bstride = seeds_pi;
+  P.dog_bstride = tot * P.ND;
+  HIPCHK(ctx->dog.ensure((size_t)tot * P.ND * nimg * sizeof(float)));
+  if (keep_gauss) HIPCHK(ctx->gauss.ensure((size_t)tot * P.NS * nimg * sizeof(float)));
+  HIPCHK(ctx->seeds.ensure((size_t)seeds_pi * nimg * sizeof(double)));
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   if (o_first > 0) {
     const Octave& of = P.oct[o_first];
@@ -427,12 +445,14 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
         P.oct[o].l64_off = l64;
         l64 += (long long)P.NS * P.oct[o].h * P.oct[o].w;
       }
-    if (l64) HIPCHK(ctx->l64.ensure((size_t)l64 * sizeof(double)));
+    if (l64) HIPCHK(ctx->l64.ensure((size_t)l64 * nimg * sizeof(double)));
     P.l64 = l64 ? ctx->l64.as<double>() : nullptr;
-    size_t vs = 0;  // the split-pass octaves run in turn on this stream: one scratch
+    P.l64_bstride = l64;
+    size_t vs = 0;  // the split-pass octaves run in turn on this stream: one scratch (per image)
     for (int o = o_first; o < P.O; ++o)
       if (gauss_vsplit(P, o)) vs = std::max(vs, (size_t)P.NS * P.oct[o].h * P.oct[o].w);
-    if (vs) HIPCHK(ctx->vsplit.ensure(vs * sizeof(double)));
+    if (vs) HIPCHK(ctx->vsplit.ensure(vs * nimg * sizeof(double)));
+    ctx->vsplit_pi = (long long)vs;
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   const double* base0 = nullptr;
@@ -480,6 +500,13 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     }
     L.l64 = P.oct[o].l64_off >= 0 ? ctx->l64.as<double>() + P.oct[o].l64_off : nullptr;
     L.vsplit = gauss_vsplit(P, o) ? ctx->vsplit.as<double>() : nullptr;
+    L.nimg = nimg;
+    L.gauss_bs = tot * P.NS;
+    L.dog_bs = tot * P.ND;
+    L.seed_bs = seeds_pi;
+    L.base_bs = o == 0 ? 0 : seeds_pi;
+    L.l64_bs = P.l64_bstride;
+    L.vsplit_bs = ctx->vsplit_pi;
     HIPCHK(launch_gauss_dog(P, L, ctx->stream));
     if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev_go[o], ctx->stream));
@@ -677,10 +704,16 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
     words += (long long)P.S * P.oct[o].h * nw;
     rows += (long long)P.S * P.oct[o].h;
   }
+  // A batch (P.nimg images) repeats the per-image words and rows image-major.
+  const int ni = std::max(1, P.nimg);
+  ctx->xl.words_per_img = words;
+  ctx->xl.rows_per_img = (int)rows;
+  words *= ni;
+  rows *= ni;
   ctx->x_rows = rows;
   {  // capacities: an estimate for this geometry, grown on overflow (settle_extrema)
-    const long long est = std::min<long long>(std::max<long long>((long long)P.S * total_plane_px(ctx) / 192, 65536),
-                                              0x7fffffffLL);
+    const long long est = std::min<long long>(
+        std::max<long long>((long long)P.S * total_plane_px(ctx) * ni / 192, 65536), 0x7fffffffLL);
     ctx->cand_cap = std::max(ctx->cand_cap, (unsigned)est);
     ctx->amb_cap = std::max(ctx->amb_cap, 4096 + (unsigned)est / 16);
   }
@@ -711,7 +744,11 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   ctx->counters_zeroed = true;
   HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), st));
   ExtremaLaunch& L = ctx->xl;
+  const long long wpi = L.words_per_img;
+  const int rpi = L.rows_per_img;
   L = ExtremaLaunch{};
+  L.words_per_img = wpi;
+  L.rows_per_img = rpi;
   L.exact_planes = exact_planes;
   L.c_lo = exact_planes ? t_up : t_dn;
   L.c_hi = exact_planes ? t_up : std::nextafter(t_up, INFINITY);
@@ -757,7 +794,8 @@ static int extrema_finish(sift_ctx* ctx) {
       E.ww[o] = ctx->x_ww[o];
       E.woff[o] = ctx->x_woff[o];
     }
-    E.row_off[P.O] = (int)rows;
+    E.row_off[P.O] = ctx->xl.rows_per_img;
+    E.words_per_img = ctx->xl.words_per_img;
     E.bitmap = ctx->bitmap.as<unsigned long long>();
     E.rowcount = ctx->rowcount.as<unsigned>();
     E.rowoff = ctx->rowoff.as<unsigned>();
@@ -790,7 +828,8 @@ static int extrema_finish(sift_ctx* ctx) {
       E.ww[o] = ctx->x_ww[o];
       E.woff[o] = ctx->x_woff[o];
     }
-    E.row_off[P.O] = (int)rows;
+    E.row_off[P.O] = ctx->xl.rows_per_img;
+    E.words_per_img = ctx->xl.words_per_img;
     E.bitmap = ctx->lowbitmap.as<unsigned long long>();
     E.rowcount = ctx->lowrowcount.as<unsigned>();
     E.rowoff = ctx->lowrowoff.as<unsigned>();
@@ -815,6 +854,8 @@ static int extrema_finish(sift_ctx* ctx) {
   if (xpos) {  // list positions from the emission geometry instead of a binary search
     X.bitmap = ctx->bitmap.as<unsigned long long>();
     X.rowoff = ctx->rowoff.as<unsigned>();
+    X.words_per_img = ctx->xl.words_per_img;
+    X.rows_per_img = ctx->xl.rows_per_img;
     for (int o = 0; o < P.O; ++o) {
       X.row_off[o] = (int)ctx->x_row_off[o];
       X.word_off[o] = ctx->x_word_off[o];
@@ -923,7 +964,53 @@ static int refine_enqueue(sift_ctx* ctx) {
     R.counters = cnt;
     R.perm = nullptr;
     static const int band_order = exp_knob("SIFT_BAND_ORDER", 1);
-    if (band_order && ctx->slots_rows) {
+    // strip order (SIFT_REFINE_STRIP = bitmap words per strip, 0 = whole
+    // rows: band order): pieces (octave, band, strip, scale, row)
+    static const int strip_words = exp_knob("SIFT_REFINE_STRIP", 0);
+    if (band_order && ctx->slots_rows && strip_words > 0) {
+      BandOrder B{};
+      B.n_oct = P.O;
+      B.S = P.S;
+      B.strip_words = strip_words;
+      int pieces = 0;
+      for (int o = 0; o < P.O; ++o) {
+        B.piece_off[o] = pieces;
+        B.row_off[o] = (int)ctx->x_row_off[o];
+        B.nw[o] = ctx->x_nw[o];
+        B.word_off[o] = ctx->x_word_off[o];
+        B.nstrip[o] = (ctx->x_nw[o] + strip_words - 1) / strip_words;
+        pieces += ((P.oct[o].h + kBandRows - 1) / kBandRows) * B.nstrip[o] * P.S * kBandRows;
+      }
+      B.piece_off[P.O] = pieces;
+      B.row_off[P.O] = ctx->xl.rows_per_img;
+      B.rows_per_img = ctx->xl.rows_per_img;
+      B.words_per_img = ctx->xl.words_per_img;
+      B.n_rows = ctx->xl.rows_per_img * std::max(1, P.nimg);
+      pieces *= std::max(1, P.nimg);
+      B.n_items = pieces;
+      HIPCHK(ctx->band_cnt.ensure((size_t)pieces * sizeof(unsigned)));
+      HIPCHK(ctx->band_first.ensure((size_t)pieces * sizeof(unsigned)));
+      HIPCHK(ctx->band_start.ensure((size_t)pieces * sizeof(unsigned)));
+      HIPCHK(ctx->perm.ensure((size_t)cap * sizeof(unsigned)));
+      B.bitmap = ctx->bitmap.as<unsigned long long>();
+      B.rowoff = ctx->rowoff.as<unsigned>();
+      B.count = ctx->band_cnt.as<unsigned>();
+      B.first = ctx->band_first.as<unsigned>();
+      B.start = ctx->band_start.as<unsigned>();
+      B.perm = ctx->perm.as<unsigned>();
+      B.cap = cap;
+      HIPCHK(hipMemsetAsync(B.count, 0, (size_t)pieces * sizeof(unsigned), ctx->stream));
+      HIPCHK(launch_strip_pieces(P, B, ctx->stream));
+      size_t tb = 0;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, B.count, ctx->band_start.as<unsigned>(), pieces,
+                                              ctx->stream));
+      HIPCHK(ctx->temp.ensure(tb));
+      tb = ctx->temp.bytes;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, B.count, ctx->band_start.as<unsigned>(), pieces,
+                                              ctx->stream));
+      HIPCHK(launch_piece_fill(B, ctx->stream));
+      R.perm = B.perm;
+    } else if (band_order && ctx->slots_rows) {
       BandOrder B{};
       B.n_oct = P.O;
       B.S = P.S;
@@ -934,6 +1021,8 @@ static int refine_enqueue(sift_ctx* ctx) {
         items += P.S * ((P.oct[o].h + kBandRows - 1) / kBandRows);
       }
       B.item_off[P.O] = items;
+      B.rows_per_img = ctx->xl.rows_per_img;
+      items *= std::max(1, P.nimg);  // image-major
       B.n_items = items;
       HIPCHK(ctx->band_cnt.ensure((size_t)items * sizeof(unsigned)));
       HIPCHK(ctx->band_first.ensure((size_t)items * sizeof(unsigned)));
@@ -980,7 +1069,9 @@ static int refine_enqueue(sift_ctx* ctx) {
     }
   }
   ctx->has_origins = (ctx->p.flags & SIFT_F_KEYPOINT_ORIGINS) != 0;
-  HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, kCntAll * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+  // the counts and the kept keypoints per block (the block starts stay on the device)
+  const int nblk = std::max(1, P.nimg) * P.O * P.S;
+  HIPCHK(hipMemcpyAsync(ctx->h_counters, cnt, (kBlk + nblk) * sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev[6], ctx->stream));
   return SIFT_OK;
 }
@@ -1001,7 +1092,7 @@ static int refine_settle(sift_ctx* ctx) {
   ctx->n_exact += h[kCntUnc];
   ctx->n_kp = cap > 0 ? h[kCntKp] : 0;
   ctx->n_sing = h[kCntSing];
-  ctx->blk_counts.assign((size_t)ctx->P.O * ctx->P.S, 0);
+  ctx->blk_counts.assign((size_t)std::max(1, ctx->P.nimg) * ctx->P.O * ctx->P.S, 0);
   if (cap > 0)
     for (size_t b = 0; b < ctx->blk_counts.size(); ++b) ctx->blk_counts[b] = h[kBlk + b];
   if (exp_knob("SIFT_DEBUG_REFINE", 0))
@@ -1028,6 +1119,7 @@ extern "C" {
 
 int sift_copy_candidates(sift_ctx* ctx, sift_extremum* out, size_t cap, size_t* n_out) {
   if (!ctx) return SIFT_E_ARG;
+  if (ctx->P.nimg > 1) return set_err(ctx, SIFT_E_UNSUPPORTED, "a batch detection returns keypoints only");
   if (!ctx->have_cand) return set_err(ctx, SIFT_E_STATE, "no candidates");
   if (n_out) *n_out = ctx->n_cand;
   if (!out) return SIFT_OK;
@@ -1197,9 +1289,10 @@ int sift_refine(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_out, si
 // Two phases: the Gaussian+DoG pass, then extrema + refinement (the caller
 // may order the second phase after other contexts' work in between).
 static int detect_begin(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H, size_t stride,
-                        const sift_params* p) {
+                        const sift_params* p, int nimg = 1, size_t img_bstride = 0) {
   if (!ctx) return SIFT_E_ARG;
-  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, 0, nullptr, nullptr, true);
+  int rc = build_common(ctx, img_host, img_dev, W, H, stride, p, nullptr, 0, nullptr, nullptr, nimg == 1, nimg,
+                        img_bstride);
   if (rc) return rc;
   ctx->begin_pending = true;
   ctx->detect_host_img = img_host != nullptr;
@@ -1218,8 +1311,8 @@ static int detect_end(sift_ctx* ctx) {
 }
 
 static int detect_enqueue(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
-                          size_t stride, const sift_params* p) {
-  const int rc = detect_begin(ctx, img_host, img_dev, W, H, stride, p);
+                          size_t stride, const sift_params* p, int nimg = 1, size_t img_bstride = 0) {
+  const int rc = detect_begin(ctx, img_host, img_dev, W, H, stride, p, nimg, img_bstride);
   return rc ? rc : detect_end(ctx);
 }
 
@@ -1262,6 +1355,24 @@ int sift_detect_device_async(sift_ctx* ctx, const float* d_img, int width, int h
   if (ctx->detect_pending || ctx->begin_pending)
     return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
   return detect_enqueue(ctx, nullptr, d_img, width, height, stride_px, p);
+}
+
+int sift_detect_batch_device_async(sift_ctx* ctx, const float* d_imgs, int n_images, size_t image_stride_px,
+                                   int width, int height, size_t stride_px, const sift_params* p) {
+  if (!ctx) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  if (n_images < 1 || (n_images > 1 && image_stride_px < (size_t)height * stride_px))
+    return set_err(ctx, SIFT_E_ARG, "n_images < 1 or overlapping images");
+  if (ctx->detect_pending || ctx->begin_pending)
+    return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
+  return detect_enqueue(ctx, nullptr, d_imgs, width, height, stride_px, p, n_images, image_stride_px);
+}
+
+int sift_detect_batch_device(sift_ctx* ctx, const float* d_imgs, int n_images, size_t image_stride_px, int width,
+                             int height, size_t stride_px, const sift_params* p, sift_keypoint* out, size_t cap,
+                             size_t* n_out) {
+  const int rc = sift_detect_batch_device_async(ctx, d_imgs, n_images, image_stride_px, width, height, stride_px, p);
+  return rc ? rc : detect_finish(ctx, out, cap, n_out);
 }
 
 int sift_detect_begin_async(sift_ctx* ctx, const float* d_img, int width, int height, size_t stride_px,

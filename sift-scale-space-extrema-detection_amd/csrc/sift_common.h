@@ -59,20 +59,32 @@ struct Pyramid {
   double pix_thr;        // 0.8 * thr   (sift.js:285-294)
   double thr;            // thr         (background.js:572)
   int row0;              // input row of the input's first row (a row-band crop; 0 = whole image)
+  // A batch of nimg independent images of the same geometry (sift_detect_batch_device):
+  // image b's input, seeds, DoG and fp64 planes start b * *_bstride elements
+  // after image 0's, and its candidate keys b * kpi after (keys per image).
+  int nimg;
+  unsigned kpi;
+  long long img_bstride, seed_bstride, dog_bstride, l64_bstride;
   Octave oct[kMaxOctaves];
 };
 
-// Base pixel of octave o at (y, x), coordinates already clamped to the plane.
-__device__ __forceinline__ double base_at(const Pyramid& P, int o, int y, int x) {
-  if (o == 0) return (double)P.img[(long long)(y >> 1) * P.img_stride + (x >> 1)];
-  return P.seeds[P.oct[o].seed_off + (long long)y * P.oct[o].w + x];
+// Base pixel of octave o of image b at (y, x), coordinates already clamped to the plane.
+__device__ __forceinline__ double base_at(const Pyramid& P, int b, int o, int y, int x) {
+  if (o == 0) return (double)P.img[b * P.img_bstride + (long long)(y >> 1) * P.img_stride + (x >> 1)];
+  return P.seeds[b * P.seed_bstride + P.oct[o].seed_off + (long long)y * P.oct[o].w + x];
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// Candidate sort key -> (octave, scale, y, x).
-__device__ __forceinline__ void decode_key(const Pyramid& P, unsigned key, int& o, int& s, int& y,
+// Candidate sort key -> (image, octave, scale, y, x): key = b kpi + the
+// image-local key of (o, s, y, x).
+__device__ __forceinline__ void decode_key(const Pyramid& P, unsigned key, int& b, int& o, int& s, int& y,
                                            int& x) {
+  b = 0;
+  if (P.nimg > 1) {
+    b = (int)(key / P.kpi);
+    key -= (unsigned)b * P.kpi;
+  }
   o = 0;
   while (o + 1 < P.O && key >= P.oct[o + 1].key_off) ++o;
   unsigned r = key - P.oct[o].key_off;

@@ -126,7 +126,7 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
 }
 
 template <int NP, bool LOWL>
-__device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int o, int s_first, int xw,
+__device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int b, int o, int s_first, int xw,
                                        int y0, int y1) {
   const Octave& oc = P.oct[o];
   XUnit<NP> U;
@@ -143,14 +143,16 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   U.xoff = 4u * (unsigned)clampi(x, 0, oc.w - 1);
   U.plane_bytes = (unsigned)(4 * U.plane);
   U.colmask = __ballot(U.lane >= 1 && U.lane <= kXW && x >= 1 && x <= oc.w - 2);
-  U.base = P.dog + oc.dog_off + (long long)(s_first - 1) * U.plane;
+  U.base = P.dog + b * P.dog_bstride + oc.dog_off + (long long)(s_first - 1) * U.plane;
   U.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(U.base), 0, -1, 0x00020000);
-  U.key_base = oc.key_off + (unsigned)(s_first - 1) * (unsigned)U.plane;
-  U.bitmap = L.bitmap + L.word_off[o] + (long long)(s_first - 1) * oc.h * U.nw;
-  U.rowcount = L.rowcount + L.row_off[o] + (s_first - 1) * oc.h;
+  U.key_base = (unsigned)b * P.kpi + oc.key_off + (unsigned)(s_first - 1) * (unsigned)U.plane;
+  const long long wb = b * L.words_per_img + L.word_off[o] + (long long)(s_first - 1) * oc.h * U.nw;
+  const long long rb = (long long)b * L.rows_per_img + L.row_off[o] + (s_first - 1) * oc.h;
+  U.bitmap = L.bitmap + wb;
+  U.rowcount = L.rowcount + rb;
   if (LOWL) {
-    U.lowbitmap = L.lowbitmap + L.word_off[o] + (long long)(s_first - 1) * oc.h * U.nw;
-    U.lowrowcount = L.lowrowcount + L.row_off[o] + (s_first - 1) * oc.h;
+    U.lowbitmap = L.lowbitmap + wb;
+    U.lowrowcount = L.lowrowcount + rb;
   }
   U.low = 0;
 
@@ -203,8 +205,12 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
     const int nb = (int)gridDim.x, q = nb >> 3, rm = nb & 7, xc = lb & 7;
     lb = xc * q + min(xc, rm) + (lb >> 3);
   }
-  const int u = L.u_begin + lb * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (u >= L.u_end) return;
+  // units of image b: b * span + (u - u_begin), span = u_end - u_begin
+  const int span = L.u_end - L.u_begin;
+  const int ug = lb * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (ug >= span * P.nimg) return;
+  const int b = ug / span;
+  const int u = L.u_begin + ug - b * span;
   int o = 0;
   while (o + 1 < L.n_oct && u >= L.unit_off[o + 1]) ++o;
   int loc = u - L.unit_off[o];
@@ -217,11 +223,11 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
   const int s_first = 1 + g * per + min(g, rem);
   const int cnt = per + (g < rem ? 1 : 0);
   switch (cnt) {
-    case 1: x_scan<3, LOWL>(P, L, o, s_first, xw, y0, y1); break;
-    case 2: x_scan<4, LOWL>(P, L, o, s_first, xw, y0, y1); break;
-    case 3: x_scan<5, LOWL>(P, L, o, s_first, xw, y0, y1); break;
-    case 4: x_scan<6, LOWL>(P, L, o, s_first, xw, y0, y1); break;
-    default: x_scan<7, LOWL>(P, L, o, s_first, xw, y0, y1); break;
+    case 1: x_scan<3, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
+    case 2: x_scan<4, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
+    case 3: x_scan<5, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
+    case 4: x_scan<6, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
+    default: x_scan<7, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
   }
 }
 
@@ -230,23 +236,25 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
 // (ambiguous ones get their exact fp64 value from k_exact_extrema).
 __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch E) {
   const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row
-  if (g >= E.row_off[E.n_oct]) return;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row (image-major)
+  const int rpi = E.row_off[E.n_oct];
+  if (g >= rpi * P.nimg) return;
+  const int b = g / rpi, gl = g - b * rpi;
   int o = 0;
-  while (o + 1 < E.n_oct && g >= E.row_off[o + 1]) ++o;
+  while (o + 1 < E.n_oct && gl >= E.row_off[o + 1]) ++o;
   const Octave& oc = P.oct[o];
   const int h = oc.h, w = oc.w;
-  const int row = g - E.row_off[o];  // (s-1)*h + y within the octave
+  const int row = gl - E.row_off[o];  // (s-1)*h + y within the octave
   const int s = row / h + 1, y = row - (s - 1) * h;
   if (y < 1 || y > h - 2) return;
   const unsigned cnt = E.rowcount[g];
   if (cnt == 0) return;
   unsigned base = E.rowoff[g];
   const long long plane = (long long)h * w;
-  const float* __restrict__ Dc = P.dog + oc.dog_off + s * plane + (long long)y * w;
-  const unsigned kbase = oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w;
+  const float* __restrict__ Dc = P.dog + b * P.dog_bstride + oc.dog_off + s * plane + (long long)y * w;
+  const unsigned kbase = (unsigned)b * P.kpi + oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w;
   const int nw = E.nw[o];
-  const unsigned long long* bm = E.bitmap + E.word_off[o] + (long long)row * nw;
+  const unsigned long long* bm = E.bitmap + b * E.words_per_img + E.word_off[o] + (long long)row * nw;
   for (int xw0 = 0; xw0 < nw; xw0 += 64) {
     const int xw = xw0 + lane;
     unsigned long long word = xw < nw ? bm[xw] : 0ull;
@@ -284,14 +292,14 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
   const unsigned n = min(*X.n, X.cap);
   for (unsigned j = blockIdx.x; j < n_amb; j += gridDim.x) {
     const unsigned key = X.amb_keys[j];
-    int o, s, y, x;
-    decode_key(P, key, o, s, y, x);
+    int b, o, s, y, x;
+    decode_key(P, key, b, o, s, y, x);
     // position of key in the ordered candidate list
     unsigned idx;
     if (X.bitmap) {  // the row's offset + the candidate bits before x (parallel loads, one wave reduction)
       const int h = P.oct[o].h;
       const int rr = (s - 1) * h + y;
-      const long long wbase = X.word_off[o] + (long long)rr * X.nw[o];
+      const long long wbase = b * X.words_per_img + X.word_off[o] + (long long)rr * X.nw[o];
       const int xr = x - X.woff[o], xw = xr / X.ww[o], b = xr - xw * X.ww[o];
       unsigned c = 0;
       for (int w = (int)threadIdx.x; w <= xw; w += 64) {
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
       }
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
-      idx = X.rowoff[X.row_off[o] + rr] + c;
+      idx = X.rowoff[(long long)b * X.rows_per_img + X.row_off[o] + rr] + c;
     } else {  // binary search
       unsigned lo = 0, hi = n;
       while (lo < hi) {
@@ -313,7 +321,7 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
     double* d27 = smem;
     double* Lbuf = smem + 32;
     double* sh = smem + 32 + 40;
-    wave_dog_patch(P, o, s, y, x, sh, Lbuf, d27);
+    wave_dog_patch(P, b, o, s, y, x, sh, Lbuf, d27);
     if (threadIdx.x == 0 && idx < n && X.keys[idx] == key) {
       const double v = d27[13];
       bool gt = false, lt = false;
@@ -374,13 +382,14 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, xlds);
     if (e != hipSuccess) return e;
   }
-  if (L.lowbitmap) hipLaunchKernelGGL(k_extrema<true>, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), xlds, st, P, L);
-  else hipLaunchKernelGGL(k_extrema<false>, dim3((L.u_end - L.u_begin + 3) / 4), dim3(256), xlds, st, P, L);
+  const int nu = (L.u_end - L.u_begin) * std::max(1, P.nimg);
+  if (L.lowbitmap) hipLaunchKernelGGL(k_extrema<true>, dim3((nu + 3) / 4), dim3(256), xlds, st, P, L);
+  else hipLaunchKernelGGL(k_extrema<false>, dim3((nu + 3) / 4), dim3(256), xlds, st, P, L);
   return hipGetLastError();
 }
 
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st) {
-  const int rows = E.row_off[E.n_oct];
+  const int rows = E.row_off[E.n_oct] * std::max(1, P.nimg);
   if (rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_emit, dim3((rows + 3) / 4), dim3(256), 0, st, P, E);
   return hipGetLastError();

@@ -102,6 +102,8 @@ constexpr int kBW0 = kGX / 2 + kUR + 4;  // staged octave-0 region width (input 
 constexpr int kPFV = 12;             // rows in flight, vertical pass from global memory
 constexpr int kPFL = 4;              // rows in flight, vertical pass from LDS
 constexpr int kPFH = 3;              // 16-byte reads in flight, horizontal pass
+constexpr int kVertNO = 16;          // k_gauss_vert: rows per wave
+constexpr int kVertRows = 4 * kVertNO;  // ... per block
 
 __host__ __device__ constexpr int fl2(int a) { return a >> 1; }   // floor(a / 2)
 __host__ __device__ constexpr int cl2(int a) { return (a + 1) >> 1; }  // ceil(a / 2), a >= 0
@@ -337,6 +339,47 @@ struct VChunk {
         if (!(FIRST && k < t) && k - t <= M) f(k, t);
   }
 };
+// NO outputs per lane (k_gauss_vert: 16 rows per wave, half the window
+// rows loaded per output): rows k <= M + NO - 1, the same skips.
+template <int M, int NO>
+struct VChunkN {
+  static constexpr int kRows = M + NO < 8 ? M + NO : 8;
+  template <bool FIRST, class Fma>
+  __device__ __forceinline__ static void run(Fma&& f) {
+#pragma unroll
+    for (int k = 0; k < kRows; ++k)
+#pragma unroll
+      for (int t = 0; t < NO; ++t)
+        if (!(FIRST && k < t) && k - t <= M) f(k, t);
+  }
+};
+// m = 2r - jb (even): one body per tail (no zero taps at all: a chunk of 16
+// outputs would spend most of a tail's 128 pairs on them).
+template <bool FIRST, class Body>
+__device__ __forceinline__ void vchunk16_dispatch(int m, Body&& body) {
+  using F = std::integral_constant<bool, FIRST>;
+  using N = std::integral_constant<bool, false>;
+  if (FIRST) {
+    if (m >= 7) body(VChunkN<7, 16>{}, F{});
+    else body(VChunkN<7, 16>{}, N{});  // 2r < 7: zero-padded taps on both sides
+    return;
+  }
+  switch (m >= 7 ? 7 : m) {
+    case 7: body(VChunkN<7, 16>{}, N{}); break;
+    case 6: body(VChunkN<6, 16>{}, N{}); break;
+    case 4: body(VChunkN<4, 16>{}, N{}); break;
+    case 2: body(VChunkN<2, 16>{}, N{}); break;
+    case 0: body(VChunkN<0, 16>{}, N{}); break;
+    case -2: body(VChunkN<-2, 16>{}, N{}); break;
+    case -4: body(VChunkN<-4, 16>{}, N{}); break;
+    case -6: body(VChunkN<-6, 16>{}, N{}); break;
+    case -8: body(VChunkN<-8, 16>{}, N{}); break;
+    case -10: body(VChunkN<-10, 16>{}, N{}); break;
+    case -12: body(VChunkN<-12, 16>{}, N{}); break;
+    default: body(VChunkN<-14, 16>{}, N{}); break;
+  }
+}
+
 // m = 2r - jb (even).  Full chunks, and tail chunks with m >= 0, run all 64
 // (k, t) pairs (a tail's few taps past 2r are zero padding); the first chunk
 // skips its k < t triangle, the last chunks with m < 0 their rows past the
@@ -371,30 +414,38 @@ __device__ __forceinline__ void vert_glob_gen2(const GTile& T, int r, const cdou
   const int x = T.x0 - r + 2 * p;
   const int xoff = clampi(x, 0, T.w - 2) * 8;
   const bool lo_edge = x < 0, hi_edge = x >= T.w - 1;
+  // Tiles whose strip columns all lie inside the plane (wave-uniform) skip
+  // the edge selects (4 VALU per 16-byte row), as in vert_glob2.
+  const bool interior = T.x0 - r >= 0 && T.x0 + kGX + r <= T.w;
   double a0[8], a1[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
-  auto chunk = [&](int jb, auto C, auto first) {
-    using CC = decltype(C);
-    double2 v[8];
+  auto sweep = [&](auto edge) {
+    auto chunk = [&](int jb, auto C, auto first) {
+      using CC = decltype(C);
+      double2 v[8];
 #pragma unroll
-    for (int k = 0; k < CC::kRows; ++k) {
-      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
-          T.rsrc, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, T.h - 1) * T.w * 8), 0);
-      const double2 d = __builtin_bit_cast(double2, q);
-      v[k] = make_double2(hi_edge ? d.y : d.x, lo_edge ? d.x : d.y);
-    }
-    const cdouble* w = wp + jb;
-    CC::template run<decltype(first)::value>([&](int k, int t) {
-      a0[t] = fma((double)w[k - t], v[k].x, a0[t]);
-      a1[t] = fma((double)w[k - t], v[k].y, a1[t]);
-    });
-    pin(a0);
-    pin(a1);
+      for (int k = 0; k < CC::kRows; ++k) {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(
+            T.rsrc, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, T.h - 1) * T.w * 8), 0);
+        const double2 d = __builtin_bit_cast(double2, q);
+        if constexpr (decltype(edge)::value) v[k] = make_double2(hi_edge ? d.y : d.x, lo_edge ? d.x : d.y);
+        else v[k] = d;
+      }
+      const cdouble* w = wp + jb;
+      CC::template run<decltype(first)::value>([&](int k, int t) {
+        a0[t] = fma((double)w[k - t], v[k].x, a0[t]);
+        a1[t] = fma((double)w[k - t], v[k].y, a1[t]);
+      });
+      pin(a0);
+      pin(a1);
+    };
+    vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
+    for (int jb = 8; jb < NJ; jb += 8)
+      vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
   };
-  vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
-  for (int jb = 8; jb < NJ; jb += 8)
-    vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
+  if (interior) sweep(std::false_type{});
+  else sweep(std::true_type{});
   double* Vw = V + 8 * T.wv * T.sw + 2 * p;
 #pragma unroll
   for (int t = 0; t < 8; ++t) *reinterpret_cast<double2*>(Vw + t * T.sw) = make_double2(a0[t], a1[t]);
@@ -439,23 +490,28 @@ __device__ __forceinline__ void vert_glob_gen(const GTile& T, int r, const cdoub
 // kernel's own.  The tile kernel then copies its strip (vert_copy).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_gauss_vert(const Pyramid P, int o, const double* __restrict__ base,
-                                                    double* __restrict__ vout) {
+                                                    double* __restrict__ vout, long long bstride,
+                                                    long long vstride) {
   const Octave& oc = P.oct[o];
-  // largest radius (longest chains) first: blocks are dispatched in z order
-  const int s = (int)gridDim.z - 1 - (int)blockIdx.z;
+  // z = image * NS + (NS - 1 - scale): largest radius (longest chains) first,
+  // blocks are dispatched in z order
+  const int im = (int)blockIdx.z / P.NS;
+  const int s = P.NS - 1 - ((int)blockIdx.z - im * P.NS);
+  base += im * bstride;
+  vout += im * vstride;
   const int r = oc.rad[s], h = oc.h, w = oc.w;
   const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int x = blockIdx.x * kGX + lane;
-  const int y0 = blockIdx.y * kGY + 8 * wv;
+  const int y0 = blockIdx.y * kVertRows + kVertNO * wv;
   if (y0 >= h) return;  // wave-uniform
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, h * w * 8,
                                                                       0x00020000);
   const int xoff = min(x, w - 1) * 8;
-  const int NJ = 2 * r + 8, yb = y0 - r;
-  double acc[8];
+  const int NJ = 2 * r + kVertNO, yb = y0 - r;
+  double acc[kVertNO];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+  for (int t = 0; t < kVertNO; ++t) acc[t] = 0.0;
   auto chunk = [&](int jb, auto C, auto first) {
     using CC = decltype(C);
     double v[8];
@@ -466,13 +522,16 @@ __global__ __launch_bounds__(256) void k_gauss_vert(const Pyramid P, int o, cons
     CC::template run<decltype(first)::value>([&](int k, int t) { acc[t] = fma((double)wq[k - t], v[k], acc[t]); });
     pin(acc);
   };
-  vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
+  // 16 rows per wave: the window's 2r + 16 rows serve 16 outputs (2r + 8
+  // for 8 before: 12.75 -> 6.9 loads per output at r = 47), the same fma
+  // chain per output (taps in increasing order from 0.0).
+  vchunk16_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
   for (int jb = 8; jb < NJ; jb += 8)
-    vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
+    vchunk16_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
   if (x < w) {
     double* dst = vout + (long long)s * h * w + (long long)y0 * w + x;
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < kVertNO; ++t)
       if (y0 + t < h) dst[(long long)t * w] = acc[t];
   }
 }
@@ -921,11 +980,23 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
   // over the 8 XCDs; with xcd_band, XCD k runs the k-th contiguous range of
   // tiles (a band of tile rows), so the base rows its vertical passes re-read
   // stay in its own L2.  Groups of one tile are adjacent (same base region).
+  // Batch (L.nimg images of one geometry): blocks of image im follow those
+  // of image im - 1; its planes, base and seeds are im * (stride) further.
   int lb = blockIdx.x;
+  const int bpi = L.gx * L.gy * L.G;  // blocks per image
   if (L.xcd_band) {
-    const int nb = L.gx * L.gy * L.G, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    const int nb = bpi * L.nimg, q = nb >> 3, rm = nb & 7, xc = lb & 7;
     lb = xc * q + min(xc, rm) + (lb >> 3);
   }
+  const int im = lb / bpi;
+  lb -= im * bpi;
+  float* const L_gauss = L.gauss ? L.gauss + im * L.gauss_bs : nullptr;
+  float* const L_dog = L.dog + im * L.dog_bs;
+  double* const L_next_seed = L.next_seed ? L.next_seed + im * L.seed_bs : nullptr;
+  const double* const L_base = L.base ? L.base + im * L.base_bs : nullptr;
+  double* const L_l64 = L.l64 ? L.l64 + im * L.l64_bs : nullptr;
+  const double* const L_vsplit = L.vsplit ? L.vsplit + im * L.vsplit_bs : nullptr;
+  const float* const img_b = OCT0 ? P.img + im * P.img_bstride : nullptr;
   const int bz = lb % L.G, bt = lb / L.G;
   const int bx = bt % L.gx, by = bt / L.gx + L.by0;
   GTile T;
@@ -962,7 +1033,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
   T.sw = SWC > 0 ? SWC : L.sw;
   T.hrm = cl2(oc.rmax);
   if (!OCT0)
-    T.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L.base), 0, T.h * T.w * 8, 0x00020000);
+    T.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, T.h * T.w * 8, 0x00020000);
   // One strip: every wave writes (vertical pass) and reads (horizontal pass)
   // only its own 8 strip rows.
   const int nstrip = kGY * T.sw;
@@ -987,7 +1058,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
     double* S0 = smem + nstrip;
     const int kk = clampi(k0 + T.lane, 0, P.W - 1);
     for (int rr = T.wv; rr < nr; rr += 4) {
-      const float* src = P.img + (long long)clampi(q0 + rr, 0, P.H - 1) * P.img_stride;
+      const float* src = img_b + (long long)clampi(q0 + rr, 0, P.H - 1) * P.img_stride;
       if (T.lane < nc) S0[rr * kBW0 + T.lane] = (double)src[kk];
     }
   }
@@ -1037,9 +1108,9 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
       const unsigned pb = (unsigned)plane * 4u;
       const bool stor = s >= s_begin && st;
       const __amdgpu_buffer_rsrc_t rg =
-          __builtin_amdgcn_make_buffer_rsrc(L.gauss ? L.gauss + s * plane : L.dog, 0, pb, 0x00020000);
+          __builtin_amdgcn_make_buffer_rsrc(L_gauss ? L_gauss + s * plane : L_dog, 0, pb, 0x00020000);
       const __amdgpu_buffer_rsrc_t rd =
-          __builtin_amdgcn_make_buffer_rsrc(L.dog + (s > 0 ? s - 1 : 0) * plane, 0, pb, 0x00020000);
+          __builtin_amdgcn_make_buffer_rsrc(L_dog + (s > 0 ? s - 1 : 0) * plane, 0, pb, 0x00020000);
       horz96s_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V,
                    [&](int i, const double (&o)[4]) {
                      double d[4];
@@ -1049,16 +1120,16 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
                      const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
                      if (stor) {
                        if (L.vec) {
-                         if (L.gauss) bstore4(rg, voff[i], o);
+                         if (L_gauss) bstore4(rg, voff[i], o);
                          if (s > 0) bstore4(rd, voff[i], d);
                        } else if (own[i]) {
                          const long long pp = (long long)y * T.w + x;
-                         if (L.gauss) store4(L.gauss + s * plane + pp, o, nvalid);
-                         if (s > 0) store4(L.dog + (s - 1) * plane + pp, d, nvalid);
+                         if (L_gauss) store4(L_gauss + s * plane + pp, o, nvalid);
+                         if (s > 0) store4(L_dog + (s - 1) * plane + pp, d, nvalid);
                        }
                      }
-                     if (s == P.S && L.next_seed && s >= s_begin && own[i] && !(y & 1)) {
-                       double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+                     if (s == P.S && L_next_seed && s >= s_begin && own[i] && !(y & 1)) {
+                       double* sd = L_next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
                        sd[0] = o[0];
                        if (nvalid > 2) sd[1] = o[2];
                      }
@@ -1075,7 +1146,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
       horz96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V, out);
     } else {
       if constexpr (!OCT0) {
-        if (L.vsplit) vert_copy(Ts, oc.rad[s], L.vsplit + (long long)s * plane, V);
+        if (L_vsplit) vert_copy(Ts, oc.rad[s], L_vsplit + (long long)s * plane, V);
         else vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
       } else {
         vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
@@ -1093,13 +1164,13 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
     if (s >= s_begin && (st || out[0][0] == 12345.0)) {
       if (L.vec) {
         const unsigned pb = (unsigned)plane * 4u;
-        if (L.gauss) {
-          const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L.gauss + s * plane, 0, pb, 0x00020000);
+        if (L_gauss) {
+          const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000);
 #pragma unroll
           for (int i = 0; i < NI; ++i) bstore4(rg, voff[i], out[i]);
         }
         if (s > 0) {
-          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L.dog + (s - 1) * plane, 0, pb, 0x00020000);
+          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000);
 #pragma unroll
           for (int i = 0; i < NI; ++i) bstore4(rd, voff[i], d[i]);
         }
@@ -1110,8 +1181,8 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
           const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
           if (own[i]) {
             const long long pp = (long long)y * T.w + x;
-            if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
-            if (s > 0) store4(L.dog + (s - 1) * plane + pp, d[i], nvalid);
+            if (L_gauss) store4(L_gauss + s * plane + pp, out[i], nvalid);
+            if (s > 0) store4(L_dog + (s - 1) * plane + pp, d[i], nvalid);
           }
         }
       }
@@ -1133,8 +1204,8 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
         }
       }
     }
-    if (L.l64 && s >= s_begin) {  // fp64 plane for the exact passes
-      double* lp = L.l64 + s * plane;
+    if (L_l64 && s >= s_begin) {  // fp64 plane for the exact passes
+      double* lp = L_l64 + s * plane;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int y = T.y0 + 8 * T.wv + irw(i);
@@ -1146,13 +1217,13 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
         }
       }
     }
-    if (s == P.S && L.next_seed && s >= s_begin) {
+    if (s == P.S && L_next_seed && s >= s_begin) {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int y = T.y0 + 8 * T.wv + irw(i);
         const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
         if (own[i] && !(y & 1)) {
-          double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+          double* sd = L_next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
           sd[0] = out[i][0];
           if (nvalid > 2) sd[1] = out[i][2];
         }
@@ -1827,8 +1898,10 @@ int gauss_tile_rows(const Pyramid& P, int o) { return (P.oct[o].h + kGY - 1) / k
 hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin, int ty_end) {
   static_assert(kGY == kGaussTileRows, "tile rows");
   const Octave& oc = P.oct[L.o];
+  if (L.nimg < 1) L.nimg = 1;
   if (L.fuse && !gauss_can_fuse(P, L.o)) return hipErrorInvalidValue;
-  if (const size_t lb = ty_end < 0 && !L.fuse ? lds_path_bytes(P, L.o) : 0) {
+  if (L.nimg > 1 && (L.fuse || ty_end >= 0)) return hipErrorInvalidValue;  // batches: whole octaves, no fused decisions
+  if (const size_t lb = ty_end < 0 && !L.fuse && L.nimg == 1 ? lds_path_bytes(P, L.o) : 0) {
     static bool lattr = false;
     if (!lattr) {
       (void)hipFuncSetAttribute((const void*)k_gauss_lds<96, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1880,7 +1953,7 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
   static const int xband = exp_knob("SIFT_XCD_BAND", -1);
   static const int xband0 = exp_knob("SIFT_XCD_BAND0", 0);
   L.xcd_band = L.o >= 1 ? ((xband >> (L.o - 1)) & 1) : xband0;
-  const dim3 grid(L.gx * L.gy * L.G);
+  const dim3 grid(L.gx * L.gy * L.G * L.nimg);
   const size_t lds = gauss_lds_bytes(P, L.o, L.fuse != 0);
   static bool attr_set = false;
   if (!attr_set) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
@@ -1900,13 +1973,13 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
   L.zero = oc.rmax > (staged0(P, L.o) ? kUR : kUR1) ? 1 : 0;
   if (L.vsplit) {
     if (L.o == 0 || !L.base) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_gauss_vert, dim3((oc.w + kGX - 1) / kGX, (oc.h + kGY - 1) / kGY, P.NS), dim3(256), 0, st, P,
-                       L.o, L.base, L.vsplit);
+    hipLaunchKernelGGL(k_gauss_vert, dim3((oc.w + kGX - 1) / kGX, (oc.h + kVertRows - 1) / kVertRows, P.NS * L.nimg),
+                       dim3(256), 0, st, P, L.o, L.base, L.vsplit, L.base_bs, L.vsplit_bs);
   }
   // Producer / consumer waves (k_gauss_ws) for octaves >= 1 whose two
   // strips fit the CU's LDS (SIFT_GAUSS_WS=0: k_gauss_dog, A/B builds).
   static const int ws = exp_knob("SIFT_GAUSS_WS", 0);
-  if (ws && L.o >= 1 && !L.fuse && ty_end < 0 && oc.w >= 2 && 2 * lds <= 160 * 1024) {
+  if (ws && L.nimg == 1 && L.o >= 1 && !L.fuse && ty_end < 0 && oc.w >= 2 && 2 * lds <= 160 * 1024) {
     static bool wattr = false;
     if (!wattr) {
       (void)hipFuncSetAttribute((const void*)k_gauss_ws<96, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -52,6 +52,10 @@ struct GaussLaunch {
   int gx, gy, G;      // tiles per row, tile rows, scale groups (1D grid of gx gy G blocks)
   int by0;            // first tile row of this launch (a band of tile rows by0 .. by0 + gy - 1)
   int xcd_band;       // 1: block -> tile so that each XCD runs a contiguous band of tile rows
+  // batch: nimg images in one launch (blocks image-major); image im's
+  // pointers are the fields above + im * these element strides
+  int nimg;
+  long long gauss_bs, dog_bs, seed_bs, base_bs, l64_bs, vsplit_bs;
 };
 
 constexpr int kXW = 62;      // output columns per extrema wave (lanes 1..62; lanes 0, 63 are halo)
@@ -81,6 +85,8 @@ struct ExtremaLaunch {
   unsigned amb_cap;
   unsigned long long* lowbitmap; // certain low-contrast extrema, same layout as bitmap (nullptr = not listed)
   unsigned* lowrowcount;
+  long long words_per_img;       // batch (P.nimg images): image b's words / rows start b * these after image 0's
+  int rows_per_img;
 };
 
 // One launch over every octave: global row g (one wave each) = row_off[o] +
@@ -101,6 +107,7 @@ struct EmitLaunch {
   unsigned cap;                  // slots in keys/value/keep (overflow is detected by the host)
   int deferred;                  // 1: value = NaN ("the fp32 plane value"): the refinement reads it from its
                                  // patch, launch_fill_values before the list is copied out; no plane gather here
+  long long words_per_img;       // batch: bitmap words per image (rows per image = row_off[n_oct])
 };
 
 // Fills the deferred (NaN) candidate values of slots [0, *n) from the DoG planes.
@@ -126,6 +133,8 @@ struct ExactLaunch {
   int row_off[kMaxOctaves];
   long long word_off[kMaxOctaves];
   int nw[kMaxOctaves], ww[kMaxOctaves], woff[kMaxOctaves];
+  long long words_per_img;       // batch: bitmap words / rows per image
+  int rows_per_img;
 };
 
 struct RefineLaunch {
@@ -155,14 +164,28 @@ constexpr int kBandRows = SIFT_BAND_ROWS;
 struct BandOrder {
   int n_oct, S, n_items;
   int item_off[kMaxOctaves + 1];  // first item of each octave: items (band, scale) of octave o
-  int row_off[kMaxOctaves];       // first global row (o, s = 1, y = 0) of each octave in rowoff
+  int row_off[kMaxOctaves + 1];   // first global row (o, s = 1, y = 0) of each octave in rowoff
   const unsigned* rowoff;         // exclusive scan of the extrema stage's row counts
   unsigned* count;                // per item: slots in it
   unsigned* first;                // per item: its first slot
   const unsigned* start;          // per item: exclusive scan of count (first position in the new order)
   unsigned* perm;                 // out: position -> slot
   int cap;
+  int rows_per_img;               // batch: rowoff rows per image (items are image-major, item_off per image)
+  // Strip order (strip_words > 0): pieces (octave, band, strip of strip_words
+  // bitmap words, scale, band row) instead of items (octave, band, scale), so
+  // the candidates whose patches share DoG lines are a few slots apart.
+  int strip_words;
+  int piece_off[kMaxOctaves + 1];  // first piece of each octave (per image)
+  int nstrip[kMaxOctaves];         // strips per row
+  int nw[kMaxOctaves];             // bitmap words per row
+  long long word_off[kMaxOctaves]; // first bitmap word of each octave
+  long long words_per_img;
+  const unsigned long long* bitmap;
+  int n_rows;                      // rows (o, s, y) of all images: one wave each in k_strip_pieces
 };
+hipError_t launch_strip_pieces(const Pyramid& P, const BandOrder& B, hipStream_t st);
+hipError_t launch_piece_fill(const BandOrder& B, hipStream_t st);
 hipError_t launch_band_items(const Pyramid& P, const BandOrder& B, hipStream_t st);
 hipError_t launch_band_fill(const Pyramid& P, const BandOrder& B, hipStream_t st);
 
@@ -214,7 +237,8 @@ hipError_t launch_scatter_keypoints(const unsigned* keep, const unsigned* pos, c
 // candidate list at blk[kBlkStart + b], b = o * S + s - 1 (candidates are in
 // key order, so a block is a slot range), or sets blk[kBlkUnsorted] when the
 // list is not in key order.
-constexpr int kBlkN = kMaxOctaves * kMaxScales;   // blk[b]: kept keypoints of block b (launch_count_keypoints)
+constexpr int kBlkN = 1024;  // blk[b]: kept keypoints of block b = (image, octave, scale) (launch_count_keypoints)
+static_assert(kBlkN >= kMaxOctaves * kMaxScales, "one image's blocks");
 constexpr int kBlkStart = kBlkN;                  // blk[kBlkStart + b], b <= O*S: first slot of block b
 constexpr int kBlkUnsorted = kBlkStart + kBlkN + 1;
 constexpr int kBlkWords = kBlkUnsorted + 1;

@@ -280,12 +280,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   if (i < n && L.keep && !L.keep[i]) {
     L.status[i] = kRefDiscard;
   } else if (i < n) {
-    int o, s, m, n;
-    decode_key(P, L.cand_key[i], o, s, m, n);
+    int b, o, s, m, n;
+    decode_key(P, L.cand_key[i], b, o, s, m, n);
     const Octave& oc = P.oct[o];
     const int h = oc.h, w = oc.w;
     const long long plane = (long long)h * w;
-    const float* __restrict__ D = P.dog + oc.dog_off;
+    const float* __restrict__ D = P.dog + b * P.dog_bstride + oc.dog_off;
     double value = L.cand_val[i];
     if (value != value) value = (double)D[s * plane + (long long)m * w + n];  // deferred: the fp32 plane value
     const double dval = EXACT ? 0.0 : fabs(value) * 0x1p-24;
@@ -365,8 +365,8 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
   for (unsigned j = blockIdx.x; j < nu; j += gridDim.x) {
     const unsigned e = L.uncertain[j];
     const unsigned i = e & ~kPolish;
-    int o, s, m, n;
-    decode_key(P, L.cand_key[i], o, s, m, n);
+    int b, o, s, m, n;
+    decode_key(P, L.cand_key[i], b, o, s, m, n);
     const Octave& oc = P.oct[o];
     double* d27 = smem;
     double* Lbuf = smem + 32;
@@ -374,11 +374,11 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
     double value = 0;
     int status = kRefDiscard;
     if (e & kPolish) {
-      wave_dog_patch(P, o, s, m, n, sh, Lbuf, d27);
+      wave_dog_patch(P, b, o, s, m, n, sh, Lbuf, d27);
       value = d27[13];  // all lanes: d27 is visible after the patch's barrier
       const Keypoint& k = L.kp[i];
       const int s1 = k.scale_level, m1 = k.local_y, n1 = k.local_x;
-      if (s1 != s || m1 != m || n1 != n) wave_dog_patch(P, o, s1, m1, n1, sh, Lbuf, d27);
+      if (s1 != s || m1 != m || n1 != n) wave_dog_patch(P, b, o, s1, m1, n1, sh, Lbuf, d27);
       if (threadIdx.x == 0) {
         const StepOut R = refine_step<false>(d27, o, s1, m1, n1, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr,
                                              false, 0.0);
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
       // not kept on exact values (cannot happen with certain decisions): the whole chain
     }
     for (int it = 0; it < 5; ++it) {
-      wave_dog_patch(P, o, s, m, n, sh, Lbuf, d27);
+      wave_dog_patch(P, b, o, s, m, n, sh, Lbuf, d27);
       if (threadIdx.x == 0) {
         if (it == 0) value = d27[13];  // exact fp64 candidate value (:565 uses it)
         const StepOut R = refine_step<false>(d27, o, s, m, n, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr, it == 4,
@@ -425,10 +425,11 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
   }
 }
 
+// Block of a key: (image, octave, scale), image-major.
 __device__ __forceinline__ int key_block(const Pyramid& P, unsigned key) {
-  int o, s, y, x;
-  decode_key(P, key, o, s, y, x);
-  return o * P.S + (s - 1);
+  int b, o, s, y, x;
+  decode_key(P, key, b, o, s, y, x);
+  return (b * P.O + o) * P.S + (s - 1);
 }
 
 __global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const int* __restrict__ status,
@@ -441,9 +442,9 @@ __global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const i
   const int m = (int)min(*n, (unsigned)cap);
   bool k = false;
   if (i < m) {
-    int o, s, y, x;
-    decode_key(P, key[i], o, s, y, x);
-    const int b = o * P.S + (s - 1), nb = P.O * P.S;
+    int im, o, s, y, x;
+    decode_key(P, key[i], im, o, s, y, x);
+    const int b = (im * P.O + o) * P.S + (s - 1), nb = P.nimg * P.O * P.S;
     k = status[i] == kRefKeep;
     if (k && own_lo >= 0) {  // row-band ownership by candidate row (octave o rows: 2 r at o = 0, r >> (o-1))
       const int yw = y + ((P.row0 * 2) >> o);
@@ -489,7 +490,7 @@ __global__ __launch_bounds__(256) void k_count_kp(const Pyramid P, const unsigne
                                                   unsigned* __restrict__ out, unsigned* __restrict__ blk) {
   __shared__ unsigned hist[kBlkN];
   const unsigned m = min(*n, cap);
-  const int nb = P.O * P.S;
+  const int nb = P.nimg * P.O * P.S;
   auto kept_before = [&](unsigned j) { return j < cap ? pos[j] : pos[cap - 1] + keep[cap - 1]; };
   if (threadIdx.x == 0) *out = m ? kept_before(m) : 0u;
   if (!m) return;  // blk[b] stays 0
@@ -511,8 +512,8 @@ __global__ __launch_bounds__(256) void k_decode_origins(const Pyramid P, const u
                                                         int32_t* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  int o, s, y, x;
-  decode_key(P, keys[i], o, s, y, x);
+  int b, o, s, y, x;
+  decode_key(P, keys[i], b, o, s, y, x);
   out[4 * i + 0] = o;
   out[4 * i + 1] = s;
   out[4 * i + 2] = y + ((P.row0 * 2) >> o);
@@ -566,10 +567,10 @@ __global__ __launch_bounds__(256) void k_fill_values(const Pyramid P, const unsi
   if (i >= (int)min(*n, (unsigned)cap)) return;
   const double v = value[i];
   if (v == v) return;
-  int o, s, y, x;
-  decode_key(P, keys[i], o, s, y, x);
+  int b, o, s, y, x;
+  decode_key(P, keys[i], b, o, s, y, x);
   const Octave& oc = P.oct[o];
-  value[i] = (double)P.dog[oc.dog_off + (long long)s * oc.h * oc.w + (long long)y * oc.w + x];
+  value[i] = (double)P.dog[b * P.dog_bstride + oc.dog_off + (long long)s * oc.h * oc.w + (long long)y * oc.w + x];
 }
 
 hipError_t launch_fill_values(const Pyramid& P, const unsigned* keys, double* value, const unsigned* n, int cap,
@@ -584,13 +585,15 @@ hipError_t launch_fill_values(const Pyramid& P, const unsigned* keys, double* va
 __global__ __launch_bounds__(256) void k_band_items(const Pyramid P, const BandOrder B) {
   const int it = blockIdx.x * 256 + threadIdx.x;
   if (it >= B.n_items) return;
+  const int ipi = B.item_off[B.n_oct];  // items per image (image-major)
+  const int im = it / ipi, il = it - im * ipi;
   int o = 0;
-  while (o + 1 < B.n_oct && it >= B.item_off[o + 1]) ++o;
-  const int loc = it - B.item_off[o];
+  while (o + 1 < B.n_oct && il >= B.item_off[o + 1]) ++o;
+  const int loc = il - B.item_off[o];
   const int b = loc / B.S, s = loc % B.S + 1;
   const int h = P.oct[o].h;
   const int y0 = b * kBandRows, y1 = min(h, y0 + kBandRows);
-  const int r0 = B.row_off[o] + (s - 1) * h + y0;
+  const long long r0 = (long long)im * B.rows_per_img + B.row_off[o] + (s - 1) * h + y0;
   const unsigned f = B.rowoff[r0];
   B.first[it] = f;
   B.count[it] = B.rowoff[r0 + (y1 - y0)] - f;
@@ -603,6 +606,76 @@ __global__ __launch_bounds__(256) void k_band_fill(const Pyramid P, const BandOr
   const unsigned c = B.count[it], f = B.first[it], st = B.start[it];
   for (unsigned j = threadIdx.x & 63; j < c; j += 64)
     if (st + j < (unsigned)B.cap) B.perm[st + j] = f + j;
+}
+
+// Strip order pieces: one wave per row (image, octave, scale, y) of the
+// extrema stage.  Its bitmap words give each strip's candidate count and the
+// slot of its first candidate (row offset + the candidates of the strips
+// before it); the piece (octave, band, strip, scale, y - band start) of the
+// new order receives them.  Pieces of rows past the plane stay zero.
+__global__ __launch_bounds__(256) void k_strip_pieces(const Pyramid P, const BandOrder B) {
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row (image-major)
+  const int lane = threadIdx.x & 63;
+  if (g >= B.n_rows) return;
+  const int rpi = B.rows_per_img;
+  const int im = g / rpi, gl = g - im * rpi;
+  int o = 0;
+  while (o + 1 < B.n_oct && gl >= B.row_off[o + 1]) ++o;
+  const int h = P.oct[o].h, nw = B.nw[o], SW = B.strip_words;
+  const int row = gl - B.row_off[o], s = row / h + 1, y = row - (s - 1) * h;
+  const int band = y / kBandRows, yb = y - band * kBandRows;
+  const unsigned long long* bm = B.bitmap + im * B.words_per_img + B.word_off[o] + (long long)row * nw;
+  const unsigned r0 = B.rowoff[g];
+  const int ppi = B.piece_off[B.n_oct];
+  // piece (band, strip, s, yb) of octave o
+  const long long pbase = (long long)im * ppi + B.piece_off[o] +
+                          ((long long)band * B.nstrip[o]) * (B.S * kBandRows) + (s - 1) * kBandRows + yb;
+  unsigned before = 0;  // candidates of the row's earlier word chunks
+  for (int w0 = 0; w0 < nw; w0 += 64) {
+    const int w = w0 + lane;
+    const unsigned c = w < nw ? (unsigned)__popcll(bm[w]) : 0u;
+    unsigned inc = c;  // inclusive wave scan
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned t = __shfl_up(inc, off);
+      if (lane >= off) inc += t;
+    }
+    // the lane holding a strip's first word writes the strip's piece: its
+    // count = inclusive sum at the strip's last word - exclusive sum at its
+    // first (64 % SW == 0: a chunk of 64 words holds whole strips)
+    const bool head = w < nw && w % SW == 0;
+    const int last = head ? min(nw - 1, w + SW - 1) - w0 : lane;
+    const unsigned end_inc = __shfl(inc, last);  // all lanes take part
+    if (head) {
+      const long long pc = pbase + (long long)(w / SW) * (B.S * kBandRows);
+      B.first[pc] = r0 + before + inc - c;
+      B.count[pc] = end_inc - (inc - c);
+    }
+    before += __shfl(inc, 63);
+  }
+}
+
+// One thread per piece (most hold 0-2 candidates): its slots in order at its
+// position of the new order.
+__global__ __launch_bounds__(256) void k_piece_fill(const BandOrder B) {
+  const int it = blockIdx.x * 256 + threadIdx.x;
+  if (it >= B.n_items) return;
+  const unsigned c = B.count[it], f = B.first[it], st = B.start[it];
+  for (unsigned j = 0; j < c; ++j)
+    if (st + j < (unsigned)B.cap) B.perm[st + j] = f + j;
+}
+
+hipError_t launch_strip_pieces(const Pyramid& P, const BandOrder& B, hipStream_t st) {
+  if (B.n_rows <= 0) return hipSuccess;
+  if (B.strip_words < 1 || 64 % B.strip_words) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_strip_pieces, dim3((B.n_rows + 3) / 4), dim3(256), 0, st, P, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_piece_fill(const BandOrder& B, hipStream_t st) {
+  if (B.n_items <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_piece_fill, dim3((B.n_items + 255) / 256), dim3(256), 0, st, B);
+  return hipGetLastError();
 }
 
 hipError_t launch_band_items(const Pyramid& P, const BandOrder& B, hipStream_t st) {

@@ -416,6 +416,13 @@ export function lastCounts(device = 0) {
   return native.counts(deviceState(device).ctx);
 }
 
+// Device stage times of the last call chain on a device (HIP events, ms:
+// gaussDogMs, extremaMs, refineMs, h2dMs, gaussOct0Ms) and the host wall
+// time of its last keypoint copy to the host (d2hMs).
+export function lastTimings(device = 0) {
+  return native.timings(deviceState(device).ctx);
+}
+
 // ---------------------------------------------------------------------------
 // Image products either side of the path (SURVEY.md §8f rows 2-3), on device.
 // ---------------------------------------------------------------------------

@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/sift_hip.h"
 
@@ -402,13 +403,32 @@ static napi_value js_refine_params(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
-static napi_value keypoints_to_js(napi_env env, struct sift_ctx *ctx, size_t n, size_t singular) {
-  sift_keypoint *tmp = (sift_keypoint *)malloc(sizeof(sift_keypoint) * (n ? n : 1));
-  int rc = sift_copy_keypoints(ctx, tmp, n, &n);
+/* Host wall time of the last keypoint copy to the host (device->host of the
+ * 48-byte records, completed before return), ms: timings().d2hMs. */
+static double g_d2h_ms = 0.0;
+
+static double now_ms(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec * 1e3 + (double)t.tv_nsec * 1e-6;
+}
+
+/* Copy of the last keypoints to a malloc'd host array (*out; NULL on error). */
+static int copy_keypoints_host(struct sift_ctx *ctx, size_t *n, sift_keypoint **out) {
+  sift_keypoint *tmp = (sift_keypoint *)malloc(sizeof(sift_keypoint) * (*n ? *n : 1));
+  const double t0 = now_ms();
+  int rc = sift_copy_keypoints(ctx, tmp, *n, n);
+  g_d2h_ms = now_ms() - t0;
   if (rc) {
     free(tmp);
-    return throw_sift(env, ctx, rc, "sift_copy_keypoints");
+    tmp = NULL;
   }
+  *out = tmp;
+  return rc;
+}
+
+/* JS arrays from host keypoint records (takes ownership of tmp). */
+static napi_value keypoint_arrays(napi_env env, sift_keypoint *tmp, size_t n, size_t singular) {
   int32_t *ints;
   double *d;
   napi_value ia = make_typed(env, napi_int32_array, 4 * n, 4, (void **)&ints);
@@ -431,6 +451,13 @@ static napi_value keypoints_to_js(napi_env env, struct sift_ctx *ctx, size_t n, 
   napi_create_double(env, (double)singular, &sv);
   napi_set_named_property(env, out, "singular", sv);
   return out;
+}
+
+static napi_value keypoints_to_js(napi_env env, struct sift_ctx *ctx, size_t n, size_t singular) {
+  sift_keypoint *tmp = NULL;
+  int rc = copy_keypoints_host(ctx, &n, &tmp);
+  if (rc) return throw_sift(env, ctx, rc, "sift_copy_keypoints");
+  return keypoint_arrays(env, tmp, n, singular);
 }
 
 /* refine(ctx) -> {ints, doubles, singular} (singular > 0: caller mirrors the reference's TypeError) */
@@ -484,12 +511,17 @@ typedef struct {
   int w, h, rc;
   sift_params p;
   size_t n;
+  sift_keypoint *kp;  /* host records, copied on the worker thread */
 } detect_job;
 
 static void detect_execute(napi_env env, void *data) {
   (void)env;
   detect_job *j = (detect_job *)data;
   j->rc = sift_detect(j->ctx, j->img, j->w, j->h, (size_t)j->w, &j->p, NULL, 0, &j->n);
+  if (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR) {
+    const int rc = copy_keypoints_host(j->ctx, &j->n, &j->kp);
+    if (rc) j->rc = rc;
+  }
 }
 
 static void detect_complete(napi_env env, napi_status status, void *data) {
@@ -498,7 +530,8 @@ static void detect_complete(napi_env env, napi_status status, void *data) {
   if (status == napi_ok && (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR)) {
     size_t sing = 0;
     sift_last_counts(j->ctx, NULL, NULL, NULL, &sing, NULL);
-    napi_value res = keypoints_to_js(env, j->ctx, j->n, sing);
+    napi_value res = keypoint_arrays(env, j->kp, j->n, sing);
+    j->kp = NULL;
     if (res) {
       napi_resolve_deferred(env, j->deferred, res);
     } else {
@@ -514,6 +547,7 @@ static void detect_complete(napi_env env, napi_status status, void *data) {
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, j->deferred, err);
   }
+  free(j->kp);
   napi_delete_reference(env, j->img_ref);
   napi_delete_reference(env, j->ctx_ref);
   napi_delete_async_work(env, j->work);
@@ -568,6 +602,30 @@ static napi_value js_counts(napi_env env, napi_callback_info info) {
   for (int i = 0; i < 5; ++i) {
     napi_value x;
     napi_create_double(env, (double)v[i], &x);
+    napi_set_named_property(env, out, names[i], x);
+  }
+  return out;
+}
+
+/* timings(ctx) -> device stage times of the last call chain (sift_last_timings)
+ * and the host wall time of the last keypoint copy to the host, ms */
+static napi_value js_timings(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  sift_timings t;
+  memset(&t, 0, sizeof t);
+  int rc = sift_last_timings(ctx, &t);
+  if (rc) return throw_sift(env, ctx, rc, "sift_last_timings");
+  const char *names[6] = {"gaussDogMs", "extremaMs", "refineMs", "h2dMs", "gaussOct0Ms", "d2hMs"};
+  const double v[6] = {t.gauss_dog_ms, t.extrema_ms, t.refine_ms, t.h2d_ms, t.gauss_oct0_ms, g_d2h_ms};
+  napi_value out;
+  napi_create_object(env, &out);
+  for (int i = 0; i < 6; ++i) {
+    napi_value x;
+    napi_create_double(env, v[i], &x);
     napi_set_named_property(env, out, names[i], x);
   }
   return out;
@@ -704,6 +762,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"detect", 0, js_detect, 0, 0, 0, napi_enumerable, 0},
       {"detectAsync", 0, js_detect_async, 0, 0, 0, napi_enumerable, 0},
       {"counts", 0, js_counts, 0, 0, 0, napi_enumerable, 0},
+      {"timings", 0, js_timings, 0, 0, 0, napi_enumerable, 0},
       {"rgbaToGray", 0, js_rgba_to_gray, 0, 0, 0, napi_enumerable, 0},
       {"buildScaleSpaceRgba", 0, js_build_rgba, 0, 0, 0, napi_enumerable, 0},
       {"detectRgba", 0, js_detect_rgba, 0, 0, 0, napi_enumerable, 0},

@@ -57,6 +57,7 @@ ABI_SYMBOLS = (
     "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device", "sift_last_octave_timings",
     "sift_detect_from_seed_range_device", "sift_merge_keypoint_blocks_device", "sift_set_owned_rows",
     "sift_last_block_counts", "sift_copy_low_contrast", "sift_set_flags",
+    "sift_detect_batch_device", "sift_detect_batch_device_async",
 )
 
 
@@ -150,6 +151,10 @@ def lib():
         "sift_detect_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_detect_device_async": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp]),
         "sift_detect_wait": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_detect_batch_device": (ctypes.c_int, [vp, vp, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int, sz, pp, vp,
+                                                    sz, szp]),
+        "sift_detect_batch_device_async": (ctypes.c_int, [vp, vp, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int, sz,
+                                                          pp]),
         "sift_detect_begin_async": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp]),
         "sift_detect_end_async": (ctypes.c_int, [vp]),
         "sift_copy_keypoint_origins_device": (ctypes.c_int, [vp, vp, sz, szp]),
@@ -438,6 +443,29 @@ class Context:
                                                      int(stride or width), ctypes.byref(params)),
                     "sift_detect_device_async")
         self.params, self.width, self.height = params, width, height
+
+    def detect_batch_device_async(self, d_ptr, n_images, width, height, params, image_stride=None, stride=None):
+        """Enqueue one detection of a batch of n_images device images (image b
+        at d_ptr + 4 * b * image_stride bytes; default height * width): ONE
+        launch per stage over the batch (sift_detect_batch_device_async);
+        finish with detect_wait(), split with batch_counts()."""
+        st = int(stride or width)
+        self._check(self._L.sift_detect_batch_device_async(self._h, ctypes.c_void_p(int(d_ptr)), int(n_images),
+                                                           int(image_stride or height * st), int(width),
+                                                           int(height), st, ctypes.byref(params)),
+                    "sift_detect_batch_device_async")
+        self.params, self.width, self.height = params, width, height
+
+    def detect_batch_device(self, d_ptr, n_images, width, height, params, image_stride=None, stride=None,
+                            raise_singular=False):
+        """Synchronous batch detection; returns the total keypoint count."""
+        self.detect_batch_device_async(d_ptr, n_images, width, height, params, image_stride, stride)
+        return self.detect_wait(raise_singular=raise_singular)
+
+    def batch_counts(self, n_images):
+        """Keypoints per image of the last batch detection (sums of its
+        image-major block counts)."""
+        return self.block_counts().reshape(int(n_images), -1).sum(axis=1)
 
     def detect_begin_async(self, d_ptr, width, height, params, stride=None):
         """Phase 1 of an asynchronous detection: the Gaussian+DoG pass."""

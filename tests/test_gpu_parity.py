@@ -521,3 +521,58 @@ def test_bench_octave0_schedule_4k_matches_sync():
     finally:
         for hip, d in bufs:
             hip.hipFree(d)
+
+
+# ---------------------------------------------------------------------------
+# Batches of independent images (BASELINE cfg 4's images per GPU): one launch
+# per stage over the batch must give every image exactly its own detection.
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("W,H,O,S,n", [
+    (1920, 1080, 4, 5, 8),   # cfg 4's per-GPU share, eight distinct images
+    (333, 517, 4, 3, 3),     # odd sizes (scalar plane stores, edge tiles)
+    (960, 540, 6, 5, 2),     # octaves 4, 5 with radii 94 / 188: split pass and kept fp64 planes per image
+])
+def test_batch_equals_single_detections(gpu_ctx, W, H, O, S, n):
+    import torch
+    p = sift_amd.make_params(O, S)
+    imgs = np.stack([blob_image(W, H, seed=100 + i) for i in range(n)])
+    d = torch.from_numpy(imgs).to("cuda:0")
+    singles, counts = [], []
+    for i in range(n):
+        gpu_ctx.detect_device(d[i].data_ptr(), W, H, p)
+        singles.append(gpu_ctx.keypoints().copy())
+        counts.append(singles[-1].shape[0])
+    total = gpu_ctx.detect_batch_device(d.data_ptr(), n, W, H, p)
+    got = gpu_ctx.keypoints()
+    assert total == sum(counts) and got.shape[0] == total
+    np.testing.assert_array_equal(gpu_ctx.batch_counts(n), counts)
+    assert got.tobytes() == np.concatenate(singles).tobytes()
+    assert len({s.tobytes() for s in singles}) == n  # distinct images, distinct lists
+    # a single image through the batch entry point is the plain detection
+    assert gpu_ctx.detect_batch_device(d[n - 1].data_ptr(), 1, W, H, p) == counts[-1]
+    assert gpu_ctx.keypoints().tobytes() == singles[-1].tobytes()
+
+
+def test_batch_async_and_padded_image_stride(gpu_ctx):
+    """The asynchronous batch entry point, images not back to back (a row
+    stride and an image stride with padding), and the unsupported options."""
+    import torch
+    W, H, n = 640, 480, 4
+    p = sift_amd.make_params(4, 3)
+    stride, istride = W + 32, (H + 5) * (W + 32)
+    buf = torch.zeros(n * istride, dtype=torch.float32, device="cuda:0")
+    singles = []
+    for i in range(n):
+        img = torch.from_numpy(blob_image(W, H, seed=200 + i)).to("cuda:0")
+        buf[i * istride:i * istride + H * stride].view(H, stride)[:, :W] = img
+        gpu_ctx.detect_device(img.data_ptr(), W, H, p)
+        singles.append(gpu_ctx.keypoints().copy())
+    torch.cuda.synchronize()
+    gpu_ctx.detect_batch_device_async(buf.data_ptr(), n, W, H, p, image_stride=istride, stride=stride)
+    gpu_ctx.detect_wait()
+    assert gpu_ctx.keypoints().tobytes() == np.concatenate(singles).tobytes()
+    with pytest.raises(sift_amd.SiftError):
+        gpu_ctx.detect_batch_device(buf.data_ptr(), n, W, H, sift_amd.make_params(4, 3, flags=sift_amd.F_LOW_CONTRAST_LIST),
+                                    image_stride=istride, stride=stride)
+    with pytest.raises(sift_amd.SiftError):  # overlapping images
+        gpu_ctx.detect_batch_device(buf.data_ptr(), n, W, H, p, image_stride=W, stride=stride)

@@ -1,0 +1,107 @@
+// Times the JavaScript drop-in (js/sift.mjs over the N-API addon over
+// libsift_hip.so) the way a Node caller of the reference's surface uses it:
+// host Float32 ImageData in, keypoints out (src/worker.js:29-98 names).
+//   1. detect(): one call, host image in -> keypoint objects out
+//   2. detectAsync(): the same on the libuv pool (a Promise per image)
+//   3. the four-stage chain of the reference: computeGaussianScaleSpace ->
+//      computeDifferenceOfGaussians -> findCandidateKeypoints ->
+//      refineCandidateKeypoints, every stage returning its host arrays
+// usage: node bench_js.mjs <image.f32> <width> <height> <octaves> <scales> <reps> <out.json>
+import fs from 'fs';
+import { performance } from 'perf_hooks';
+import * as sift from '../../sift-scale-space-extrema-detection_amd/js/sift.mjs';
+
+const [, , inPath, Ws, Hs, Os, Ss, repsS, outPath] = process.argv;
+const W = +Ws, H = +Hs, O = +Os, S = +Ss, reps = +repsS;
+const raw = fs.readFileSync(inPath);
+const data = new Float32Array(raw.buffer, raw.byteOffset, W * H);
+const image = { width: W, height: H, data };
+const opts = { number_of_octaves: O, scales_per_octave: S, min_blur_level: 0.8, assumed_blur: 0.5 };
+const mpix = W * H / 1e6;
+async function main() {
+const med = (a) => { const b = [...a].sort((x, y) => x - y); return b[b.length >> 1]; };
+const out = { width: W, height: H, octaves: O, scales: S, reps, node: process.version };
+
+// 1. detect (synchronous; the device work is serialised in the call)
+let kp = sift.detect(image, opts);  // warm-up (allocations, code objects)
+sift.detect(image, opts);
+const wall = [], tm = [];
+for (let i = 0; i < reps; i++) {
+  const t0 = performance.now();
+  kp = sift.detect(image, opts);
+  wall.push(performance.now() - t0);
+  tm.push(sift.lastTimings());
+}
+const pick = (k) => med(tm.map((t) => t[k]));
+out.detect = {
+  keypoints: kp.length, wall_ms: med(wall), mpix_per_s: mpix / (med(wall) / 1e3),
+  h2d_ms: pick('h2dMs'), gauss_dog_ms: pick('gaussDogMs'), extrema_ms: pick('extremaMs'), refine_ms: pick('refineMs'),
+  d2h_ms: pick('d2hMs'),
+  what: 'sift.detect(ImageData-shaped Float32 host image) -> keypoint objects; wall = host clock around the call '
+    + '(H2D of the image, G+DoG, extrema, refine, D2H of the 48-B records, JS objects); stage times = HIP events',
+};
+out.detect.host_other_ms = out.detect.wall_ms - (out.detect.h2d_ms + out.detect.gauss_dog_ms + out.detect.extrema_ms
+  + out.detect.refine_ms + out.detect.d2h_ms);
+
+// 2. detectAsync: one at a time, then `reps` images queued at once
+const awall = [];
+for (let i = 0; i < reps; i++) {
+  const t0 = performance.now();
+  kp = await sift.detectAsync(image, opts);
+  awall.push(performance.now() - t0);
+}
+const tq = performance.now();
+const all = await Promise.all(Array.from({ length: reps }, () => sift.detectAsync(image, opts)));
+const qms = performance.now() - tq;
+out.detectAsync = {
+  keypoints: all[0].length, wall_ms: med(awall), mpix_per_s: mpix / (med(awall) / 1e3),
+  queued_images: reps, queued_total_ms: qms, queued_mpix_per_s: reps * mpix / (qms / 1e3),
+  d2h_ms: sift.lastTimings().d2hMs,
+  what: 'await sift.detectAsync(image): the same call on the libuv pool (keypoint copy on the worker thread); '
+    + 'queued: Promise.all over reps images (jobs of one device run one after another)',
+};
+
+// 3. the reference's four stages on host arrays (ImageData-shaped planes)
+const stages = { gauss: [], dog: [], find: [], refine: [] };
+let nc = 0, nk = 0;
+for (let i = 0; i < Math.max(2, Math.min(reps, 5)); i++) {
+  let t0 = performance.now();
+  const ss = sift.computeGaussianScaleSpace({ input_image: image, ...opts });
+  stages.gauss.push(performance.now() - t0);
+  t0 = performance.now();
+  const dog = sift.computeDifferenceOfGaussians(ss);
+  stages.dog.push(performance.now() - t0);
+  t0 = performance.now();
+  const cands = sift.findCandidateKeypoints({ differenceOfGaussians: dog, scalesPerOctave: S });
+  stages.find.push(performance.now() - t0);
+  const ext = sift.lastTimings().extremaMs;
+  t0 = performance.now();
+  const ref = sift.refineCandidateKeypoints({ differenceOfGaussians: dog, scalesPerOctave: S, numberOfOctaves: O,
+    candidateKeypoints: cands, minBlurLevel: 0.8, minInterpixelDistance: 0.5 });
+  stages.refine.push(performance.now() - t0);
+  nc = 0;
+  cands.forEach((oc) => oc.forEach((sc) => { nc += sc.localExtremas.length; }));
+  nk = ref.length;
+  stages.extrema_device_ms = ext;
+}
+let planeBytes = 0;
+{
+  const dims = [];
+  for (let o = 0, h = 2 * H, w = 2 * W; o < O; o++, h = Math.ceil(h / 2), w = Math.ceil(w / 2)) dims.push(h * w);
+  planeBytes = dims.reduce((a, p) => a + 4 * p * (2 * S + 5), 0);
+}
+const sum = med(stages.gauss) + med(stages.dog) + med(stages.find) + med(stages.refine);
+out.stages = {
+  candidates: nc, keypoints: nk,
+  computeGaussianScaleSpace_ms: med(stages.gauss), computeDifferenceOfGaussians_ms: med(stages.dog),
+  findCandidateKeypoints_ms: med(stages.find), refineCandidateKeypoints_ms: med(stages.refine),
+  extrema_device_ms: stages.extrema_device_ms, total_ms: sum, mpix_per_s: mpix / (sum / 1e3),
+  planes_to_host_bytes: planeBytes,
+  what: 'the reference chain main.js -> worker stages: every Gaussian and DoG plane comes back to the host as an '
+    + 'ImageData-shaped Float32Array (the reference returns them), candidates and keypoints as JS objects; '
+    + 'the device pyramid stays resident between stages',
+};
+fs.writeFileSync(outPath, JSON.stringify(out, null, 1));
+console.log(JSON.stringify(out));
+}
+main().catch((e) => { console.error(e); process.exit(1); });
