@@ -16,14 +16,14 @@ static_assert(kExactBatch <= kWPad, "batched taps stay inside the zero padding")
 // LDS doubles one wave needs: 4 L-scales x 3 rows x (2R+3) vertical sums.
 __host__ __device__ inline int exact_scratch_doubles(int rmax) { return 12 * (2 * rmax + 3) + 36; }
 
-// DoG patch d[k][a][c] of image b for DoG scales s-1+k (k = 0..2), rows
+// DoG patch d[k][a][c] of image im for DoG scales s-1+k (k = 0..2), rows
 // y-1+a, cols x-1+c, from the L-scales s-1..s+2.  Result in lds d27[27] (visible to all
 // lanes).  Requires blockDim.x == 64 (one wave): __syncthreads() is a wave
 // barrier.  The four L-scales' vertical sums run side by side (one pass over
 // 12 (2r+3) independent fma chains), then 36 lanes form the horizontal sums:
 //   V_t[a][c] = sum_j w_j B(clamp(y-1+a-r+j), clamp(x-1-r+c))
 //   L_t[a][b] = sum_i w_i V_t[a][b + i]            (output column x-1+b)
-__device__ inline void wave_dog_patch(const Pyramid& P, int b, int o, int s, int y, int x, double* sh,
+__device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, int y, int x, double* sh,
                                       double* Lbuf /*36*/, double* d27) {
   const Octave& oc = P.oct[o];
   const int h = oc.h, w = oc.w;
@@ -32,7 +32,7 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int b, int o, int s, int
     if (lane < 27) {
       const int k = lane / 9, q = lane - 9 * k, a = q / 3, c = q - 3 * a;
       const long long plane = (long long)h * w;
-      const double* L0 = P.l64 + b * P.l64_bstride + oc.l64_off + (long long)(s - 1 + k) * plane + (long long)(y - 1 + a) * w + (x - 1 + c);
+      const double* L0 = P.l64 + im * P.l64_bstride + oc.l64_off + (long long)(s - 1 + k) * plane + (long long)(y - 1 + a) * w + (x - 1 + c);
       d27[lane] = L0[0] - L0[plane];
     }
     __syncthreads();
@@ -58,7 +58,7 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int b, int o, int s, int
     for (int jb = 0; jb <= 2 * r; jb += kExactBatch) {
       double v[kExactBatch];
 #pragma unroll
-      for (int k = 0; k < kExactBatch; ++k) v[k] = base_at(P, b, o, clampi(yb + jb + k, 0, h - 1), xx);
+      for (int k = 0; k < kExactBatch; ++k) v[k] = base_at(P, im, o, clampi(yb + jb + k, 0, h - 1), xx);
 #pragma unroll
       for (int k = 0; k < kExactBatch; ++k) acc = fma(wp[jb + k], v[k], acc);
     }

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row (image-major)
   const int rpi = E.row_off[E.n_oct];
   if (g >= rpi * P.nimg) return;
-  const int b = g / rpi, gl = g - b * rpi;
+  const int im = g / rpi, gl = g - im * rpi;
   int o = 0;
   while (o + 1 < E.n_oct && gl >= E.row_off[o + 1]) ++o;
   const Octave& oc = P.oct[o];
@@ -251,10 +251,10 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
   if (cnt == 0) return;
   unsigned base = E.rowoff[g];
   const long long plane = (long long)h * w;
-  const float* __restrict__ Dc = P.dog + b * P.dog_bstride + oc.dog_off + s * plane + (long long)y * w;
-  const unsigned kbase = (unsigned)b * P.kpi + oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w;
+  const float* __restrict__ Dc = P.dog + im * P.dog_bstride + oc.dog_off + s * plane + (long long)y * w;
+  const unsigned kbase = (unsigned)im * P.kpi + oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w;
   const int nw = E.nw[o];
-  const unsigned long long* bm = E.bitmap + b * E.words_per_img + E.word_off[o] + (long long)row * nw;
+  const unsigned long long* bm = E.bitmap + im * E.words_per_img + E.word_off[o] + (long long)row * nw;
   for (int xw0 = 0; xw0 < nw; xw0 += 64) {
     const int xw = xw0 + lane;
     unsigned long long word = xw < nw ? bm[xw] : 0ull;
@@ -292,14 +292,14 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
   const unsigned n = min(*X.n, X.cap);
   for (unsigned j = blockIdx.x; j < n_amb; j += gridDim.x) {
     const unsigned key = X.amb_keys[j];
-    int b, o, s, y, x;
-    decode_key(P, key, b, o, s, y, x);
+    int im, o, s, y, x;
+    decode_key(P, key, im, o, s, y, x);
     // position of key in the ordered candidate list
     unsigned idx;
     if (X.bitmap) {  // the row's offset + the candidate bits before x (parallel loads, one wave reduction)
       const int h = P.oct[o].h;
       const int rr = (s - 1) * h + y;
-      const long long wbase = b * X.words_per_img + X.word_off[o] + (long long)rr * X.nw[o];
+      const long long wbase = im * X.words_per_img + X.word_off[o] + (long long)rr * X.nw[o];
       const int xr = x - X.woff[o], xw = xr / X.ww[o], b = xr - xw * X.ww[o];
       unsigned c = 0;
       for (int w = (int)threadIdx.x; w <= xw; w += 64) {
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
       }
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
-      idx = X.rowoff[(long long)b * X.rows_per_img + X.row_off[o] + rr] + c;
+      idx = X.rowoff[(long long)im * X.rows_per_img + X.row_off[o] + rr] + c;
     } else {  // binary search
       unsigned lo = 0, hi = n;
       while (lo < hi) {
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
     double* d27 = smem;
     double* Lbuf = smem + 32;
     double* sh = smem + 32 + 40;
-    wave_dog_patch(P, b, o, s, y, x, sh, Lbuf, d27);
+    wave_dog_patch(P, im, o, s, y, x, sh, Lbuf, d27);
     if (threadIdx.x == 0 && idx < n && X.keys[idx] == key) {
       const double v = d27[13];
       bool gt = false, lt = false;

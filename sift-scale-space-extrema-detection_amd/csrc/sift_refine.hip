@@ -280,12 +280,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   if (i < n && L.keep && !L.keep[i]) {
     L.status[i] = kRefDiscard;
   } else if (i < n) {
-    int b, o, s, m, n;
-    decode_key(P, L.cand_key[i], b, o, s, m, n);
+    int im, o, s, m, n;
+    decode_key(P, L.cand_key[i], im, o, s, m, n);
     const Octave& oc = P.oct[o];
     const int h = oc.h, w = oc.w;
     const long long plane = (long long)h * w;
-    const float* __restrict__ D = P.dog + b * P.dog_bstride + oc.dog_off;
+    const float* __restrict__ D = P.dog + im * P.dog_bstride + oc.dog_off;
     double value = L.cand_val[i];
     if (value != value) value = (double)D[s * plane + (long long)m * w + n];  // deferred: the fp32 plane value
     const double dval = EXACT ? 0.0 : fabs(value) * 0x1p-24;
@@ -365,8 +365,8 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
   for (unsigned j = blockIdx.x; j < nu; j += gridDim.x) {
     const unsigned e = L.uncertain[j];
     const unsigned i = e & ~kPolish;
-    int b, o, s, m, n;
-    decode_key(P, L.cand_key[i], b, o, s, m, n);
+    int im, o, s, m, n;
+    decode_key(P, L.cand_key[i], im, o, s, m, n);
     const Octave& oc = P.oct[o];
     double* d27 = smem;
     double* Lbuf = smem + 32;
@@ -374,11 +374,11 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
     double value = 0;
     int status = kRefDiscard;
     if (e & kPolish) {
-      wave_dog_patch(P, b, o, s, m, n, sh, Lbuf, d27);
+      wave_dog_patch(P, im, o, s, m, n, sh, Lbuf, d27);
       value = d27[13];  // all lanes: d27 is visible after the patch's barrier
       const Keypoint& k = L.kp[i];
       const int s1 = k.scale_level, m1 = k.local_y, n1 = k.local_x;
-      if (s1 != s || m1 != m || n1 != n) wave_dog_patch(P, b, o, s1, m1, n1, sh, Lbuf, d27);
+      if (s1 != s || m1 != m || n1 != n) wave_dog_patch(P, im, o, s1, m1, n1, sh, Lbuf, d27);
       if (threadIdx.x == 0) {
         const StepOut R = refine_step<false>(d27, o, s1, m1, n1, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr,
                                              false, 0.0);
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
       // not kept on exact values (cannot happen with certain decisions): the whole chain
     }
     for (int it = 0; it < 5; ++it) {
-      wave_dog_patch(P, b, o, s, m, n, sh, Lbuf, d27);
+      wave_dog_patch(P, im, o, s, m, n, sh, Lbuf, d27);
       if (threadIdx.x == 0) {
         if (it == 0) value = d27[13];  // exact fp64 candidate value (:565 uses it)
         const StepOut R = refine_step<false>(d27, o, s, m, n, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr, it == 4,
@@ -427,9 +427,9 @@ __global__ __launch_bounds__(64) void k_refine_exact(const Pyramid P, const Refi
 
 // Block of a key: (image, octave, scale), image-major.
 __device__ __forceinline__ int key_block(const Pyramid& P, unsigned key) {
-  int b, o, s, y, x;
-  decode_key(P, key, b, o, s, y, x);
-  return (b * P.O + o) * P.S + (s - 1);
+  int im, o, s, y, x;
+  decode_key(P, key, im, o, s, y, x);
+  return (im * P.O + o) * P.S + (s - 1);
 }
 
 __global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const int* __restrict__ status,
@@ -512,8 +512,8 @@ __global__ __launch_bounds__(256) void k_decode_origins(const Pyramid P, const u
                                                         int32_t* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  int b, o, s, y, x;
-  decode_key(P, keys[i], b, o, s, y, x);
+  int im, o, s, y, x;
+  decode_key(P, keys[i], im, o, s, y, x);
   out[4 * i + 0] = o;
   out[4 * i + 1] = s;
   out[4 * i + 2] = y + ((P.row0 * 2) >> o);
@@ -567,10 +567,10 @@ __global__ __launch_bounds__(256) void k_fill_values(const Pyramid P, const unsi
   if (i >= (int)min(*n, (unsigned)cap)) return;
   const double v = value[i];
   if (v == v) return;
-  int b, o, s, y, x;
-  decode_key(P, keys[i], b, o, s, y, x);
+  int im, o, s, y, x;
+  decode_key(P, keys[i], im, o, s, y, x);
   const Octave& oc = P.oct[o];
-  value[i] = (double)P.dog[b * P.dog_bstride + oc.dog_off + (long long)s * oc.h * oc.w + (long long)y * oc.w + x];
+  value[i] = (double)P.dog[im * P.dog_bstride + oc.dog_off + (long long)s * oc.h * oc.w + (long long)y * oc.w + x];
 }
 
 hipError_t launch_fill_values(const Pyramid& P, const unsigned* keys, double* value, const unsigned* n, int cap,
