@@ -623,6 +623,7 @@ __global__ __launch_bounds__(256) void k_strip_pieces(const Pyramid P, const Ban
   while (o + 1 < B.n_oct && gl >= B.row_off[o + 1]) ++o;
   const int h = P.oct[o].h, nw = B.nw[o], SW = B.strip_words;
   const int row = gl - B.row_off[o], s = row / h + 1, y = row - (s - 1) * h;
+  if (y < 1 || y > h - 2) return;  // border rows: no candidates, their bitmap words are never written
   const int band = y / kBandRows, yb = y - band * kBandRows;
   const unsigned long long* bm = B.bitmap + im * B.words_per_img + B.word_off[o] + (long long)row * nw;
   const unsigned r0 = B.rowoff[g];

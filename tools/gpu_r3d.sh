@@ -2,15 +2,19 @@
 # Round 3, call d: full GPU suite (incl. batch tests), cfg4 batched vs per-image,
 # JS drop-in bench, stage-API extrema probe, cfg5 shard model + trace.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R || exit 1
+if [ "${SKIP_PYTEST:-0}" != 1 ]; then
 echo "[$(date +%T)] pytest -m gpu"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_r3d.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error|assert" $O/pytest_r3d.log | head -30; tail -30 $O/pytest_r3d.log; exit 1; }
 tail -1 $O/pytest_r3d.log
+fi
+if [ "${SKIP_CFG4:-0}" != 1 ]; then
 echo "[$(date +%T)] cfg4: 1080p x 8 per GPU"
 for a in "--batch-mode launch" "--batch-mode launch --inflight 2" "--batch-mode launch --inflight 4" "--batch-mode images" "--batch-mode images --inflight 4"; do
   timeout -k 10 200 python bench.py --width 1920 --height 1080 --batch 8 --steps 30 --warmup 5 --no-cpu-baseline --sustain-s 0 $a > $O/cfg4.json 2> $O/cfg4.err || { echo "cfg4 $a failed"; tail -5 $O/cfg4.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/cfg4.json')); r=d['roofline']; print('[$a]', d['value'], d['ms_per_step'], 'pass', r['launch_ms'], round(r['frac'],3), [round(o['iso_ms'],4) for o in r['per_octave']], 'verified', d['verified'])"
   cp $O/cfg4.json "$O/cfg4_$(echo $a | tr ' -' '__').json"
 done
+fi
 echo "[$(date +%T)] strip-ordered refinement: parity subset, then A/B"
 SIFT_HIP_LIB=$R/build_var/exp3.so SIFT_REFINE_STRIP=4 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "cfg3 or golden or reference_itself or batch" > $O/pytest_strip.log 2>&1 || { echo "pytest strip failed"; tail -30 $O/pytest_strip.log; exit 1; }
 tail -1 $O/pytest_strip.log
