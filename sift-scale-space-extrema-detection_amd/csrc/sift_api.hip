@@ -105,6 +105,8 @@ struct sift_ctx {
   long long vsplit_pi = 0;                     // ... doubles per image of a batch
   std::vector<double> wts_host;                // taps last uploaded to wts
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
+  DBuf ambbitmap;                              // ambiguous words (k_exact_words)
+  bool x_words = false;                        // this extrema stage lists ambiguous words, not keys
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
   DBuf lowbitmap, lowrowcount, lowrowoff;      // low-contrast list (SIFT_F_LOW_CONTRAST_LIST)
   DBuf low_key, low_val, late_key, late_val;
@@ -233,7 +235,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   if (!ctx) return SIFT_E_ARG;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DBuf* bufs[] = {&ctx->img, &ctx->seeds, &ctx->base0, &ctx->l64, &ctx->vsplit, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
+  DBuf* bufs[] = {&ctx->ambbitmap, &ctx->img, &ctx->seeds, &ctx->base0, &ctx->l64, &ctx->vsplit, &ctx->gauss, &ctx->dog, &ctx->wts, &ctx->bitmap,
                   &ctx->rowcount, &ctx->rowoff, &ctx->amb_keys, &ctx->keep, &ctx->pos,
                   &ctx->cand_keep, &ctx->cand_key, &ctx->cand_val, &ctx->status,
                   &ctx->kp_tmp, &ctx->kp, &ctx->uncertain, &ctx->xseed, &ctx->kp_key, &ctx->counters,
@@ -761,6 +763,15 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   L.amb_keys = ctx->amb_keys.as<unsigned>();
   L.counters = cnt;
   L.amb_cap = ctx->amb_cap;
+  // Ambiguous pixels are re-decided a word (62 pixels) at a time
+  // (k_exact_words; SIFT_XWORDS=0: one wave per pixel key, experiments) --
+  // not with fused octave-0 decisions, which list keys.
+  static const int xwords = exp_knob("SIFT_XWORDS", 1);
+  ctx->x_words = xwords && nf == 0 && !exact_planes;
+  if (ctx->x_words) {
+    HIPCHK(ctx->ambbitmap.ensure((size_t)words * sizeof(unsigned long long)));
+    L.ambbitmap = ctx->ambbitmap.as<unsigned long long>();
+  }
   L.lowbitmap = ctx->want_low ? ctx->lowbitmap.as<unsigned long long>() : nullptr;
   L.lowrowcount = ctx->want_low ? ctx->lowrowcount.as<unsigned>() : nullptr;
   return SIFT_OK;
@@ -864,7 +875,23 @@ static int extrema_finish(sift_ctx* ctx) {
       X.woff[o] = ctx->x_woff[o];
     }
   }
-  HIPCHK(launch_exact_extrema(P, X, ctx->stream));
+  if (ctx->x_words) {
+    X.ambbitmap = ctx->ambbitmap.as<unsigned long long>();
+    X.bitmap = ctx->bitmap.as<unsigned long long>();
+    X.rowoff = ctx->rowoff.as<unsigned>();
+    X.words_per_img = ctx->xl.words_per_img;
+    X.rows_per_img = ctx->xl.rows_per_img;
+    for (int o = 0; o < P.O; ++o) {
+      X.row_off[o] = (int)ctx->x_row_off[o];
+      X.word_off[o] = ctx->x_word_off[o];
+      X.nw[o] = ctx->x_nw[o];
+      X.ww[o] = ctx->x_ww[o];
+      X.woff[o] = ctx->x_woff[o];
+    }
+    HIPCHK(launch_exact_words(P, X, ctx->stream));
+  } else {
+    HIPCHK(launch_exact_extrema(P, X, ctx->stream));
+  }
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   ctx->slot_cap = (int)ctx->cand_cap;
   ctx->has_keep = true;
@@ -896,7 +923,7 @@ static int settle_extrema(sift_ctx* ctx) {
   ctx->ext_pending = false;
   const unsigned n = h[kCntN], n_amb = h[kCntAmb];
   const unsigned n_ls = ctx->want_low ? h[kCntLowSure] : 0u;
-  if (n > ctx->cand_cap || n_amb > ctx->amb_cap || n_ls > ctx->low_cap) {
+  if (n > ctx->cand_cap || n_amb > ctx->amb_cap || n_ls > ctx->low_cap || h[kAmbWords] > ctx->amb_cap) {
     if (n > ctx->cand_cap) ctx->cand_cap = n + n / 4 + 1024;
     if (n_amb > ctx->amb_cap) ctx->amb_cap = n_amb + n_amb / 4 + 1024;
     if (n_ls > ctx->low_cap) ctx->low_cap = n_ls + n_ls / 4 + 1024;

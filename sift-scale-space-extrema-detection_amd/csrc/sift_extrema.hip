@@ -50,6 +50,7 @@ struct XUnit {
   unsigned long long* lowbitmap;  // the same for the certain low-contrast extrema (LOWL)
   unsigned* lowrowcount;
   unsigned low;
+  long long word0;     // index of (s_first, row 0, word 0) in L.bitmap (ambiguous word list)
 };
 
 template <int NP>
@@ -83,6 +84,7 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
   }
   unsigned wlo = 0, whi = 0, wcnt = 0;
   unsigned llo = 0, lhi = 0, lcnt = 0;  // LOWL: the low-contrast word
+  unsigned alo = 0, ahi = 0;            // the ambiguous word (L.ambbitmap)
 #pragma unroll
   for (int q = 1; q <= NP - 2; ++q) {
     const float v = Wn.cv[B][q];
@@ -90,9 +92,14 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     const float nmin = min3f(vn[q - 1], vn[q + 1], min3f(Wn.hn[A][q], Wn.hn[C][q], Wn.en[B][q]));
     const unsigned key = U.key_base + (unsigned)(q - 1) * (unsigned)U.plane + (unsigned)y * (unsigned)U.w +
                          (unsigned)(U.xw * kXW - 1 + U.lane);
-    unsigned long long lowmask;
-    const unsigned long long bit = x_row_decide(v, nmax, nmin, U.colmask, L.c_lo, L.c_hi, L.exact_planes != 0, key,
-                                                &L.counters[0], L.amb_keys, L.amb_cap, U.low, lowmask);
+    unsigned long long lowmask, ambmask;
+    const unsigned long long bit =
+        x_row_decide(v, nmax, nmin, U.colmask, L.c_lo, L.c_hi, L.exact_planes != 0, key, &L.counters[0],
+                     L.ambbitmap ? nullptr : L.amb_keys, L.amb_cap, U.low, lowmask, ambmask);
+    if (ambmask && L.ambbitmap && U.lane == q - 1) {
+      alo = (unsigned)(ambmask >> 1);
+      ahi = (unsigned)(ambmask >> 33);
+    }
     if (bit) {
       const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
       if (U.lane == q - 1) {
@@ -118,6 +125,13 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     const long long r = (long long)U.lane * U.h + y;
     U.bitmap[r * U.nw + U.xw] = ((unsigned long long)whi << 32) | wlo;
     if (wcnt) atomicAdd(&U.rowcount[r], wcnt);
+    if ((alo | ahi) && L.ambbitmap) {  // an ambiguous word (rare): its bits and its index for k_exact_words
+      const long long gw = U.word0 + r * U.nw + U.xw;
+      L.ambbitmap[gw] = ((unsigned long long)ahi << 32) | alo;
+      atomicAdd(&L.counters[0], (unsigned)(__popc(alo) + __popc(ahi)));
+      const unsigned slot = atomicAdd(&L.counters[kAmbWords], 1u);
+      if (slot < L.amb_cap) L.amb_keys[slot] = (unsigned)gw;
+    }
     if (LOWL) {
       U.lowbitmap[r * U.nw + U.xw] = ((unsigned long long)lhi << 32) | llo;
       if (lcnt) atomicAdd(&U.lowrowcount[r], lcnt);
@@ -149,6 +163,7 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   const long long wb = b * L.words_per_img + L.word_off[o] + (long long)(s_first - 1) * oc.h * U.nw;
   const long long rb = (long long)b * L.rows_per_img + L.row_off[o] + (s_first - 1) * oc.h;
   U.bitmap = L.bitmap + wb;
+  U.word0 = wb;
   U.rowcount = L.rowcount + rb;
   if (LOWL) {
     U.lowbitmap = L.lowbitmap + wb;
@@ -348,6 +363,140 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
     }
     __syncthreads();  // smem is reused by the next key
   }
+}
+
+// One wave per listed ambiguous word (persistent over the device-side
+// count): the fp64 DoG values of the word's 64 columns (62 pixels and their
+// x-1 / x+1 halo), rows y-1..y+1, DoG scales s-1..s+1, recomputed from the
+// octave base with the same sums as k_gauss_dog / wave_dog_patch (vertical
+// sums V in LDS -- every (L-scale, row, column) chain once --, then the
+// horizontal sums), or read from the kept fp64 planes (l64).  Every
+// ambiguous pixel of the word is then decided exactly, as k_exact_extrema
+// decides one key: a saturated (flat) region makes whole words ambiguous,
+// and one wave then settles 62 pixels instead of one.
+__global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const ExactLaunch X) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int lane = threadIdx.x;
+  const unsigned nwd = min(X.counters[kAmbWords], X.amb_cap);
+  const unsigned n = min(*X.n, X.cap);
+  const int VS = X.amb_lds_stride;
+  double* V = smem;              // [t * 3 + a][cc], t < 4 L-scales, a < 3 rows, cc < 64 + 2 r_t
+  double* Lb = smem + 12 * VS;   // [t * 3 + a][c], c < 64
+  for (unsigned j = blockIdx.x; j < nwd; j += gridDim.x) {
+    const long long gw = X.amb_keys[j];
+    const int im = (int)(gw / X.words_per_img);
+    const long long lw = gw - im * X.words_per_img;
+    int o = 0;
+    while (o + 1 < P.O && lw >= X.word_off[o + 1]) ++o;
+    const Octave& oc = P.oct[o];
+    const int h = oc.h, w = oc.w, nw = X.nw[o];
+    const long long rel = lw - X.word_off[o];
+    const int rr = (int)(rel / nw), xw = (int)(rel - (long long)rr * nw);
+    const int s = rr / h + 1, y = rr - (s - 1) * h;
+    const unsigned long long amb = X.ambbitmap[gw], cand = X.bitmap[gw];
+    // list slot of the row's first candidate in this word
+    unsigned c = 0;
+    for (int q = lane; q < xw; q += 64) c += (unsigned)__popcll(X.bitmap[gw - xw + q]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+    const unsigned base = X.rowoff[(long long)im * X.rows_per_img + X.row_off[o] + rr] + c;
+    const int x0 = xw * kXW - 1;  // column of lane 0 (lanes 1..62 <-> bits 0..61)
+    if (oc.l64_off >= 0) {
+      const long long plane = (long long)h * w;
+      const double* L0 = P.l64 + im * P.l64_bstride + oc.l64_off;
+      const int xx = clampi(x0 + lane, 0, w - 1);
+      for (int ta = 0; ta < 12; ++ta) {
+        const int t = s - 1 + ta / 3, a = ta % 3;
+        Lb[ta * 64 + lane] = L0[t * plane + (long long)(y - 1 + a) * w + xx];
+      }
+    } else {
+      for (int t4 = 0; t4 < 4; ++t4) {
+        const int t = s - 1 + t4, r = oc.rad[t], nc = 64 + 2 * r;
+        const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
+        for (int idx = lane; idx < 3 * nc; idx += 64) {
+          const int a = idx / nc, cc = idx - a * nc;
+          const int xx = clampi(x0 - r + cc, 0, w - 1);
+          const int yb = y - 1 + a - r;
+          double acc = 0.0;  // the chain of wave_dog_patch, term for term
+          for (int jb = 0; jb <= 2 * r; jb += kExactBatch) {
+            double v[kExactBatch];
+#pragma unroll
+            for (int k = 0; k < kExactBatch; ++k) v[k] = base_at(P, im, o, clampi(yb + jb + k, 0, h - 1), xx);
+#pragma unroll
+            for (int k = 0; k < kExactBatch; ++k) acc = fma(wp[jb + k], v[k], acc);
+          }
+          V[(t4 * 3 + a) * VS + cc] = acc;
+        }
+      }
+      __syncthreads();
+      for (int ta = 0; ta < 12; ++ta) {
+        const int t = s - 1 + ta / 3, r = oc.rad[t];
+        const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
+        const double* vr = V + ta * VS + lane;
+        double acc = 0.0;
+        for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], vr[i], acc);
+        Lb[ta * 64 + lane] = acc;
+      }
+    }
+    __syncthreads();
+    if (lane >= 1 && lane <= kXW && ((amb >> (lane - 1)) & 1ull)) {
+      auto D = [&](int k, int a, int cl) { return Lb[(k * 3 + a) * 64 + cl] - Lb[((k + 1) * 3 + a) * 64 + cl]; };
+      const double v = D(1, 1, lane);
+      bool gt = false, lt = false;
+      for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 3; ++a)
+          for (int dc = -1; dc <= 1; ++dc) {
+            if (k == 1 && a == 1 && dc == 0) continue;
+            const double d = D(k, a, lane + dc);
+            gt |= d >= v;  // a neighbour >= v rules out a strict maximum
+            lt |= d <= v;
+          }
+      const bool ext = !gt || !lt;
+      const bool cnd = ext && fabs(v) >= P.pix_thr;
+      const int bit = lane - 1;
+      const unsigned idx = base + (unsigned)__popcll(cand & ((1ull << bit) - 1ull));
+      const int x = x0 + lane;
+      const unsigned key = (unsigned)im * P.kpi + oc.key_off + (unsigned)(s - 1) * (unsigned)h * (unsigned)w +
+                           (unsigned)y * (unsigned)w + (unsigned)x;
+      if (idx < n && X.keys[idx] == key) {
+        X.keep[idx] = cnd ? 1u : 0u;
+        X.value[idx] = v;
+        if (ext && !cnd) {
+          atomicAdd(&X.counters[1], 1u);
+          if (X.late_keys) {  // decided low contrast here: joins the low-contrast list
+            const unsigned slot = atomicAdd(&X.counters[6], 1u);
+            if (slot < X.amb_cap) {
+              X.late_keys[slot] = key;
+              X.late_vals[slot] = v;
+            }
+          }
+        }
+        if (!cnd) atomicAdd(&X.counters[2], 1u);  // dropped entries
+      }
+    }
+    __syncthreads();  // smem is reused by the next word
+  }
+}
+
+size_t exact_words_lds_bytes(const Pyramid& P, int* stride) {
+  int rmax = 0;
+  for (int o = 0; o < P.O; ++o)
+    if (P.oct[o].l64_off < 0) rmax = std::max(rmax, P.oct[o].rmax);
+  *stride = 64 + 2 * rmax;
+  return sizeof(double) * (size_t)(12 * (*stride) + 12 * 64);
+}
+
+hipError_t launch_exact_words(const Pyramid& P, ExactLaunch X, hipStream_t st) {
+  const size_t lds = exact_words_lds_bytes(P, &X.amb_lds_stride);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_exact_words, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)std::min<size_t>(lds, 160 * 1024));
+    if (e != hipSuccess) return e;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+  }
+  const unsigned grid = std::max(1u, std::min(X.amb_cap, 4096u));
+  hipLaunchKernelGGL(k_exact_words, dim3(grid), dim3(64), lds, st, P, X);
+  return hipGetLastError();
 }
 
 hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, int o_begin, int o_end) {

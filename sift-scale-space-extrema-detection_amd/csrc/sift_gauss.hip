@@ -937,10 +937,11 @@ __device__ __forceinline__ void fused_decide(const Pyramid& P, const GaussLaunch
     const float v = Wn.cv[B][1];
     const float nmax = max3f(vx0, vx2, max3f(Wn.hx[A][1], Wn.hx[C][1], Wn.ex[B][1]));
     const float nmin = min3f(vn0, vn2, min3f(Wn.hn[A][1], Wn.hn[C][1], Wn.en[B][1]));
+    unsigned long long ambmask;  // (the fused path lists ambiguous keys itself)
     unsigned long long lowmask;  // the low-contrast list is not fused (build_common)
     const unsigned long long bit =
         x_row_decide(v, nmax, nmin, colmask, L.X.c_lo, L.X.c_hi, false, key0 + (unsigned)y * (unsigned)T.w,
-                     &L.X.counters[0], L.X.amb_keys, L.X.amb_cap, low, lowmask);
+                     &L.X.counters[0], L.X.amb_keys, L.X.amb_cap, low, lowmask, ambmask);
     const unsigned long long word = bit >> 1;  // lanes 1..kFX -> bits 0..kFX-1
     if (l == 0) {
       const long long row = (long long)(t - 1) * T.h + y;

@@ -87,7 +87,13 @@ struct ExtremaLaunch {
   unsigned* lowrowcount;
   long long words_per_img;       // batch (P.nimg images): image b's words / rows start b * these after image 0's
   int rows_per_img;
+  // Ambiguous words (ambbitmap != nullptr): instead of one key per ambiguous
+  // pixel, the scan writes the word's ambiguous bits to ambbitmap (same
+  // layout as bitmap) and lists the word's index (into bitmap) in amb_keys
+  // (counters[kAmbWords] of them); k_exact_words re-decides a whole word.
+  unsigned long long* ambbitmap;
 };
+constexpr int kAmbWords = 8;     // counters slot: listed ambiguous words
 
 // One launch over every octave: global row g (one wave each) = row_off[o] +
 // (s-1) h_o + y.
@@ -135,6 +141,8 @@ struct ExactLaunch {
   int nw[kMaxOctaves], ww[kMaxOctaves], woff[kMaxOctaves];
   long long words_per_img;       // batch: bitmap words / rows per image
   int rows_per_img;
+  const unsigned long long* ambbitmap;  // ambiguous words (k_exact_words; nullptr: amb_keys are pixel keys)
+  int amb_lds_stride;            // k_exact_words: doubles per vertical-sum row (64 + 2 rmax)
 };
 
 struct RefineLaunch {
@@ -222,6 +230,8 @@ hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st);
 // One wave per ambiguous candidate: fp64 pointwise recompute of the 3x3x3 DoG patch.
 // Persistent grid over the device-side count of ambiguous keys (no host sync).
 hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, hipStream_t st);
+// One wave per listed ambiguous word (ExtremaLaunch.ambbitmap mode).
+hipError_t launch_exact_words(const Pyramid& P, ExactLaunch X, hipStream_t st);
 
 hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream_t st);
 hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, hipStream_t st);

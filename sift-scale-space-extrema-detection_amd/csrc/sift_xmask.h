@@ -85,8 +85,9 @@ __device__ __forceinline__ unsigned long long x_row_decide(float v, float nmax, 
                                                            unsigned long long colmask, float c_lo, float c_hi,
                                                            bool exact_planes, unsigned key, unsigned* amb_count,
                                                            unsigned* amb_keys, unsigned amb_cap, unsigned& low,
-                                                           unsigned long long& lowmask) {
+                                                           unsigned long long& lowmask, unsigned long long& ambmask) {
   lowmask = 0ull;
+  ambmask = 0ull;
   const unsigned long long ext_any = __ballot(v >= nmax || v <= nmin) & colmask;
   if (!ext_any) return 0ull;
   const float av = __builtin_fabsf(v);
@@ -101,7 +102,8 @@ __device__ __forceinline__ unsigned long long x_row_decide(float v, float nmax, 
   const unsigned long long amb = bit & (tie | ~hi);
   low += (unsigned)__popcll(count_low);
   lowmask = count_low;
-  if (amb) {  // rare: ties / contrast within fp32 rounding of the threshold
+  ambmask = amb;
+  if (amb && amb_keys) {  // rare: ties / contrast within fp32 rounding of the threshold
     const bool mine = (amb >> (threadIdx.x & 63)) & 1ull;
     const unsigned slot = wave_append(mine, amb_count);
     if (mine && slot < amb_cap) amb_keys[slot] = key;

@@ -186,3 +186,29 @@ def test_capacity_growth_on_dense_extrema():
         assert again.tobytes() == kp.tobytes()
     finally:
         ctx.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("W,H,O,S,gain", [(1920, 1080, 4, 5, 2.0), (640, 480, 6, 3, 3.0)])
+def test_saturated_image_exact_words(gpu_ctx, W, H, O, S, gain):
+    """Clipped (saturated) regions make whole rows of flat DoG values tie in
+    fp32: every such pixel is ambiguous, and the scan lists whole ambiguous
+    words that k_exact_words re-decides in fp64 (62 pixels per wave).  The
+    candidates, the low-contrast list and the keypoints must equal the
+    oracle's in the HIP path's operation order, and the ambiguous pixels must
+    be many (the case this path is for).  640x480 O6: octaves 4 and 5 keep
+    their fp64 planes (radii above 90): the l64 branch."""
+    img = blob_image(W, H, seed=1)
+    img = (np.clip(np.rint((img - 0.5) * gain * 4096 + 2048), 0, 4096) / 4096).astype(np.float32)
+    assert (img == 0).mean() + (img == 1).mean() > 0.02
+    p = sift_amd.make_params(O, S, flags=sift_amd.F_LOW_CONTRAST_LIST)
+    kp = gpu_ctx.detect(img, p).copy()
+    cand, low, counts = gpu_ctx.candidates(), gpu_ctx.low_contrast(), gpu_ctx.counts()
+    r = orc.OracleRun(img, oracle_params(p), orc.CONV_SEPARABLE_FMA_VH, threads=host_threads())
+    print("\nsaturated %dx%d O%d S%d: %d candidates, %d low, %d keypoints, %d exact re-decisions"
+          % (W, H, O, S, cand.shape[0], low.shape[0], kp.shape[0], counts["exact"]))
+    assert counts["exact"] > 10000
+    check_candidates(cand, r.candidates())
+    check_candidates(low, r.low_contrast())
+    check_keypoints(kp, r.refined)
+    assert counts["low_contrast"] == r.n_low

@@ -19,8 +19,8 @@ import sift_amd  # noqa: E402
 from sift_amd.synth import blob_image  # noqa: E402
 
 dev = torch.device("cuda:0")
-for (W, H) in [(480, 270), (1920, 1080), (3840, 2160)]:
-    img = torch.from_numpy(blob_image(W, H, seed=1)).to(dev)
+for (W, H, seed) in [(480, 270, 1), (1920, 1080, 1), (3840, 2160, 1), (3840, 2160, 42)]:
+    img = torch.from_numpy(blob_image(W, H, seed=seed)).to(dev)
     p = sift_amd.make_params(num_octaves=4, scales_per_octave=5)
     with sift_amd.Context(0) as ctx:
         st, wall, det = [], [], []
@@ -33,5 +33,8 @@ for (W, H) in [(480, 270), (1920, 1080), (3840, 2160)]:
             st.append(ctx.timings()["extrema_ms"])
             ctx.detect_device(img.data_ptr(), W, H, p)
             det.append(ctx.timings()["extrema_ms"])
-        print("%4dx%-4d stage API sift_find_extrema: events %.4f ms, host wall %.3f ms | inside sift_detect: "
-              "events %.4f ms" % (W, H, np.median(st[2:]), np.median(wall[2:]), np.median(det[2:])), flush=True)
+        c = ctx.counts()
+        print("%4dx%-4d seed %2d stage API sift_find_extrema: events %.4f ms, host wall %.3f ms | inside sift_detect: "
+              "events %.4f ms | %d candidates, %d ambiguous (exact fp64 re-decisions)"
+              % (W, H, seed, np.median(st[2:]), np.median(wall[2:]), np.median(det[2:]), c["candidates"],
+                 c["exact"]), flush=True)
