@@ -374,6 +374,8 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
 // ambiguous pixel of the word is then decided exactly, as k_exact_extrema
 // decides one key: a saturated (flat) region makes whole words ambiguous,
 // and one wave then settles 62 pixels instead of one.
+constexpr int kWordPixelMax = 4;  // up to this many ambiguous pixels a word is settled pixel by pixel
+
 __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const ExactLaunch X) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int lane = threadIdx.x;
@@ -401,6 +403,53 @@ __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const Exact
     for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
     const unsigned base = X.rowoff[(long long)im * X.rows_per_img + X.row_off[o] + rr] + c;
     const int x0 = xw * kXW - 1;  // column of lane 0 (lanes 1..62 <-> bits 0..61)
+    // Exact decision of the pixel at lane ln (bit ln - 1) from the fp64 DoG
+    // value v and its 26 neighbours (nb(k, a, dc)), written at its slot.
+    auto settle = [&](int ln, double v, auto nb) {
+      bool gt = false, lt = false;
+      for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 3; ++a)
+          for (int dc = -1; dc <= 1; ++dc) {
+            if (k == 1 && a == 1 && dc == 0) continue;
+            const double d = nb(k, a, dc);
+            gt |= d >= v;  // a neighbour >= v rules out a strict maximum
+            lt |= d <= v;
+          }
+      const bool ext = !gt || !lt;
+      const bool cnd = ext && fabs(v) >= P.pix_thr;
+      const unsigned idx = base + (unsigned)__popcll(cand & ((1ull << (ln - 1)) - 1ull));
+      const unsigned key = (unsigned)im * P.kpi + oc.key_off + (unsigned)(s - 1) * (unsigned)h * (unsigned)w +
+                           (unsigned)y * (unsigned)w + (unsigned)(x0 + ln);
+      if (idx < n && X.keys[idx] == key) {
+        X.keep[idx] = cnd ? 1u : 0u;
+        X.value[idx] = v;
+        if (ext && !cnd) {
+          atomicAdd(&X.counters[1], 1u);
+          if (X.late_keys) {  // decided low contrast here: joins the low-contrast list
+            const unsigned slot = atomicAdd(&X.counters[6], 1u);
+            if (slot < X.amb_cap) {
+              X.late_keys[slot] = key;
+              X.late_vals[slot] = v;
+            }
+          }
+        }
+        if (!cnd) atomicAdd(&X.counters[2], 1u);  // dropped entries
+      }
+    };
+    if (__popcll(amb) <= kWordPixelMax) {
+      // a few ambiguous pixels: their 3x3x3 patches alone (wave_dog_patch,
+      // 12 (2r + 3) chains each) cost less than the word's block (12 (64 + 2r))
+      double* d27 = smem;
+      double* Lp = smem + 32;
+      double* sh = smem + 32 + 40;
+      for (unsigned long long m = amb; m; m &= m - 1) {
+        const int ln = __ffsll((long long)m);  // bit ln - 1 <-> lane ln
+        wave_dog_patch(P, im, o, s, y, x0 + ln, sh, Lp, d27);
+        if (lane == 0) settle(ln, d27[13], [&](int k, int a, int dc) { return d27[k * 9 + a * 3 + 1 + dc]; });
+        __syncthreads();  // d27 is reused by the next pixel
+      }
+      continue;
+    }
     if (oc.l64_off >= 0) {
       const long long plane = (long long)h * w;
       const double* L0 = P.l64 + im * P.l64_bstride + oc.l64_off;
@@ -441,38 +490,7 @@ __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const Exact
     __syncthreads();
     if (lane >= 1 && lane <= kXW && ((amb >> (lane - 1)) & 1ull)) {
       auto D = [&](int k, int a, int cl) { return Lb[(k * 3 + a) * 64 + cl] - Lb[((k + 1) * 3 + a) * 64 + cl]; };
-      const double v = D(1, 1, lane);
-      bool gt = false, lt = false;
-      for (int k = 0; k < 3; ++k)
-        for (int a = 0; a < 3; ++a)
-          for (int dc = -1; dc <= 1; ++dc) {
-            if (k == 1 && a == 1 && dc == 0) continue;
-            const double d = D(k, a, lane + dc);
-            gt |= d >= v;  // a neighbour >= v rules out a strict maximum
-            lt |= d <= v;
-          }
-      const bool ext = !gt || !lt;
-      const bool cnd = ext && fabs(v) >= P.pix_thr;
-      const int bit = lane - 1;
-      const unsigned idx = base + (unsigned)__popcll(cand & ((1ull << bit) - 1ull));
-      const int x = x0 + lane;
-      const unsigned key = (unsigned)im * P.kpi + oc.key_off + (unsigned)(s - 1) * (unsigned)h * (unsigned)w +
-                           (unsigned)y * (unsigned)w + (unsigned)x;
-      if (idx < n && X.keys[idx] == key) {
-        X.keep[idx] = cnd ? 1u : 0u;
-        X.value[idx] = v;
-        if (ext && !cnd) {
-          atomicAdd(&X.counters[1], 1u);
-          if (X.late_keys) {  // decided low contrast here: joins the low-contrast list
-            const unsigned slot = atomicAdd(&X.counters[6], 1u);
-            if (slot < X.amb_cap) {
-              X.late_keys[slot] = key;
-              X.late_vals[slot] = v;
-            }
-          }
-        }
-        if (!cnd) atomicAdd(&X.counters[2], 1u);  // dropped entries
-      }
+      settle(lane, D(1, 1, lane), [&](int k, int a, int dc) { return D(k, a, lane + dc); });
     }
     __syncthreads();  // smem is reused by the next word
   }
@@ -483,7 +501,7 @@ size_t exact_words_lds_bytes(const Pyramid& P, int* stride) {
   for (int o = 0; o < P.O; ++o)
     if (P.oct[o].l64_off < 0) rmax = std::max(rmax, P.oct[o].rmax);
   *stride = 64 + 2 * rmax;
-  return sizeof(double) * (size_t)(12 * (*stride) + 12 * 64);
+  return std::max(sizeof(double) * (size_t)(12 * (*stride) + 12 * 64), exact_lds_bytes(P));
 }
 
 hipError_t launch_exact_words(const Pyramid& P, ExactLaunch X, hipStream_t st) {
