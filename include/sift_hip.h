@@ -239,6 +239,11 @@ int sift_detect_wait(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_
 int sift_detect_batch_device(struct sift_ctx *ctx, const float *d_imgs, int n_images, size_t image_stride_px,
                              int width, int height, size_t stride_px, const sift_params *p,
                              sift_keypoint *out, size_t cap, size_t *n_out);
+/* The same batch from host images (image b at imgs + b * image_stride_px),
+ * uploaded image by image into the context's device buffer. */
+int sift_detect_batch(struct sift_ctx *ctx, const float *imgs, int n_images, size_t image_stride_px, int width,
+                      int height, size_t stride_px, const sift_params *p, sift_keypoint *out, size_t cap,
+                      size_t *n_out);
 int sift_detect_batch_device_async(struct sift_ctx *ctx, const float *d_imgs, int n_images,
                                    size_t image_stride_px, int width, int height, size_t stride_px,
                                    const sift_params *p);

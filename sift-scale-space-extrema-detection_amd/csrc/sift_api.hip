@@ -405,7 +405,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   const long long tot = total_plane_px(ctx);
   const bool keep_gauss = !(p->flags & SIFT_F_SKIP_GAUSS_PLANES);
   if (nimg > 1) {
-    if (o_first != 0 || img_host || !img_dev || fuse_extrema || gauss_needs_base0(P) || ctx->row0 != 0 ||
+    if (o_first != 0 || (!img_host && !img_dev) || fuse_extrema || gauss_needs_base0(P) || ctx->row0 != 0 ||
         ctx->own_lo >= 0 || (p->flags & (SIFT_F_EXPORT_NEXT_SEED | SIFT_F_LOW_CONTRAST_LIST | SIFT_F_FUSED_EXTREMA)))
       return set_err(ctx, SIFT_E_UNSUPPORTED, "batch: whole device images, plain detection only");
     if ((unsigned long long)P.kpi * (unsigned long long)nimg > 0xffffffffull ||
@@ -428,12 +428,15 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
                           seed_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, ctx->stream));
     P.img = nullptr;
     P.img_stride = 0;
-  } else if (img_host) {
-    HIPCHK(ctx->img.ensure((size_t)W * H * sizeof(float)));
-    HIPCHK(hipMemcpy2DAsync(ctx->img.p, W * sizeof(float), img_host, stride * sizeof(float),
-                            W * sizeof(float), H, hipMemcpyHostToDevice, ctx->stream));
+  } else if (img_host) {  // (a batch: image b from img_host + b * img_bstride, dense on the device)
+    HIPCHK(ctx->img.ensure((size_t)W * H * nimg * sizeof(float)));
+    for (int b = 0; b < nimg; ++b)
+      HIPCHK(hipMemcpy2DAsync(ctx->img.as<float>() + (size_t)b * W * H, W * sizeof(float),
+                              img_host + (size_t)b * img_bstride, stride * sizeof(float), W * sizeof(float), H,
+                              hipMemcpyHostToDevice, ctx->stream));
     P.img = ctx->img.as<float>();
     P.img_stride = W;
+    P.img_bstride = nimg > 1 ? (long long)W * H : 0;
   } else {
     P.img = img_dev;
     P.img_stride = (int)stride;
@@ -1393,6 +1396,18 @@ int sift_detect_batch_device_async(sift_ctx* ctx, const float* d_imgs, int n_ima
   if (ctx->detect_pending || ctx->begin_pending)
     return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
   return detect_enqueue(ctx, nullptr, d_imgs, width, height, stride_px, p, n_images, image_stride_px);
+}
+
+int sift_detect_batch(sift_ctx* ctx, const float* imgs, int n_images, size_t image_stride_px, int width, int height,
+                      size_t stride_px, const sift_params* p, sift_keypoint* out, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  if (n_images < 1 || (n_images > 1 && image_stride_px < (size_t)height * stride_px))
+    return set_err(ctx, SIFT_E_ARG, "n_images < 1 or overlapping images");
+  if (ctx->detect_pending || ctx->begin_pending)
+    return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
+  const int rc = detect_enqueue(ctx, imgs, nullptr, width, height, stride_px, p, n_images, image_stride_px);
+  return rc ? rc : detect_finish(ctx, out, cap, n_out);
 }
 
 int sift_detect_batch_device(sift_ctx* ctx, const float* d_imgs, int n_images, size_t image_stride_px, int width,

@@ -388,6 +388,32 @@ export function detect(input_image, { number_of_octaves = 5, scales_per_octave =
   return keypointsFromNative(r);
 }
 
+// A batch of independent images of one size (BASELINE cfg 4's images per
+// GPU) as ONE detection (sift_detect_batch: one launch per stage over the
+// batch); returns one keypoint list per image, each exactly what detect()
+// returns for that image.
+export function detectBatch(images, { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8,
+  assumed_blur = 0.5, min_interpixel_distance = 0.5, device = 0 } = {}) {
+  if (!images.length) return [];
+  const grays = images.map(toGray);
+  const { width, height } = grays[0];
+  if (grays.some((g) => g.width !== width || g.height !== height || g.rgba)) {
+    throw new TypeError('detectBatch: gray images of one size');
+  }
+  const n = width * height;
+  const data = new Float32Array(n * grays.length);
+  grays.forEach((g, b) => data.set(g.data.subarray(0, n), b * n));
+  const st = deviceState(device);
+  const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
+  const r = native.detectBatch(st.ctx, data, grays.length, width, height, params);
+  bump(st, 'detected', width, height, params);
+  const all = keypointsFromNative(r);
+  const out = [];
+  let at = 0;
+  for (const c of r.counts) { out.push(all.slice(at, at + c)); at += c; }
+  return out;
+}
+
 // Calls on one device are serialised: each job starts when the previous one
 // on that device has settled (Promise.all over many images is fine); a
 // synchronous call on the device while a job runs throws (SIFT_E_BUSY).

@@ -499,6 +499,51 @@ static napi_value js_detect(napi_env env, napi_callback_info info) {
   return keypoints_to_js(env, ctx, n, sing);
 }
 
+/* detectBatch(ctx, Float32Array of n images back to back, n, w, h, params) ->
+ * {ints, doubles, singular, counts}: one batched detection (sift_detect_batch),
+ * keypoints image-major, counts[b] = keypoints of image b. */
+static napi_value js_detect_batch(napi_env env, napi_callback_info info) {
+  size_t argc = 6;
+  napi_value argv[6];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  if (!ctx) return NULL;
+  size_t len = 0;
+  const float *img = (const float *)typed_data(env, argv[1], napi_float32_array, &len);
+  int32_t nimg = 0, w = 0, h = 0;
+  napi_get_value_int32(env, argv[2], &nimg);
+  napi_get_value_int32(env, argv[3], &w);
+  napi_get_value_int32(env, argv[4], &h);
+  if (!img || nimg < 1 || w < 1 || h < 1 || (size_t)nimg * (size_t)w * (size_t)h > len) {
+    napi_throw_type_error(env, NULL, "images must be a Float32Array of n*width*height gray values");
+    return NULL;
+  }
+  sift_params p;
+  read_params(env, argv[5], &p);
+  size_t n = 0;
+  int rc = sift_detect_batch(ctx, img, nimg, (size_t)w * (size_t)h, w, h, (size_t)w, &p, NULL, 0, &n);
+  if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_detect_batch");
+  size_t sing = 0;
+  sift_last_counts(ctx, NULL, NULL, NULL, &sing, NULL);
+  napi_value out = keypoints_to_js(env, ctx, n, sing);
+  if (!out) return NULL;
+  int nb = 0;
+  sift_last_block_counts(ctx, NULL, 0, &nb);
+  int64_t *blk = (int64_t *)calloc((size_t)(nb > 0 ? nb : 1), sizeof(int64_t));
+  sift_last_block_counts(ctx, blk, nb, &nb);
+  double *cnt;
+  napi_value ca = make_typed(env, napi_float64_array, (size_t)nimg, 8, (void **)&cnt);
+  const int per = nb / nimg;
+  for (int b = 0; b < nimg; ++b) {
+    double c = 0;
+    for (int q = 0; q < per; ++q) c += (double)blk[b * per + q];
+    cnt[b] = c;
+  }
+  free(blk);
+  napi_set_named_property(env, out, "counts", ca);
+  return out;
+}
+
 /* ---- detectAsync: the one-call path on the libuv pool, returns a Promise ---- */
 typedef struct {
   napi_async_work work;
@@ -761,6 +806,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"setRefineParams", 0, js_refine_params, 0, 0, 0, napi_enumerable, 0},
       {"detect", 0, js_detect, 0, 0, 0, napi_enumerable, 0},
       {"detectAsync", 0, js_detect_async, 0, 0, 0, napi_enumerable, 0},
+      {"detectBatch", 0, js_detect_batch, 0, 0, 0, napi_enumerable, 0},
       {"counts", 0, js_counts, 0, 0, 0, napi_enumerable, 0},
       {"timings", 0, js_timings, 0, 0, 0, napi_enumerable, 0},
       {"rgbaToGray", 0, js_rgba_to_gray, 0, 0, 0, napi_enumerable, 0},

@@ -57,7 +57,7 @@ ABI_SYMBOLS = (
     "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device", "sift_last_octave_timings",
     "sift_detect_from_seed_range_device", "sift_merge_keypoint_blocks_device", "sift_set_owned_rows",
     "sift_last_block_counts", "sift_copy_low_contrast", "sift_set_flags",
-    "sift_detect_batch_device", "sift_detect_batch_device_async",
+    "sift_detect_batch_device", "sift_detect_batch_device_async", "sift_detect_batch",
 )
 
 
@@ -153,6 +153,7 @@ def lib():
         "sift_detect_wait": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_detect_batch_device": (ctypes.c_int, [vp, vp, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int, sz, pp, vp,
                                                     sz, szp]),
+        "sift_detect_batch": (ctypes.c_int, [vp, vp, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_detect_batch_device_async": (ctypes.c_int, [vp, vp, ctypes.c_int, sz, ctypes.c_int, ctypes.c_int, sz,
                                                           pp]),
         "sift_detect_begin_async": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp]),
@@ -461,6 +462,21 @@ class Context:
         """Synchronous batch detection; returns the total keypoint count."""
         self.detect_batch_device_async(d_ptr, n_images, width, height, params, image_stride, stride)
         return self.detect_wait(raise_singular=raise_singular)
+
+    def detect_batch(self, imgs, params, raise_singular=False):
+        """Host batch (imgs: (n, H, W) float32): one batched detection;
+        returns the keypoints of all images (image-major, split with
+        batch_counts)."""
+        a = np.ascontiguousarray(imgs, dtype=np.float32)
+        n_img, H, W = a.shape
+        n = ctypes.c_size_t()
+        rc = self._L.sift_detect_batch(self._h, a.ctypes.data_as(ctypes.c_void_p), int(n_img), int(H * W), int(W),
+                                       int(H), int(W), ctypes.byref(params), None, 0, ctypes.byref(n))
+        if rc == SIFT_E_SINGULAR and not raise_singular:
+            rc = SIFT_OK
+        self._check(rc, "sift_detect_batch")
+        self.params, self.width, self.height = params, W, H
+        return self.keypoints()
 
     def batch_counts(self, n_images):
         """Keypoints per image of the last batch detection (sums of its

@@ -52,6 +52,21 @@ if (mode !== 'schedule-only') {
   out.lowContrastCount = c3.lowContrastCount;
   out.lowContrastCountDefault = cands.lowContrastCount;
   // one-call path and its async twin
+  // a batch of the image and its mirror: each list equals its own detect()
+  {
+    const opts = { number_of_octaves: P.num_octaves, scales_per_octave: P.scales_per_octave,
+      min_blur_level: P.min_blur, assumed_blur: P.assumed_blur };
+    const mirror = new Float32Array(P.width * P.height);
+    for (let y = 0; y < P.height; y++) for (let x = 0; x < P.width; x++) {
+      mirror[y * P.width + x] = data[y * P.width + (P.width - 1 - x)];
+    }
+    const image2 = { width: P.width, height: P.height, data: mirror };
+    const batch = sift.detectBatch([image, image2, image], opts);
+    const singles = [sift.detect(image, opts), sift.detect(image2, opts)];
+    out.batchCounts = batch.map((l) => l.length);
+    out.batchEqual = JSON.stringify(batch[0]) === JSON.stringify(singles[0]) &&
+      JSON.stringify(batch[1]) === JSON.stringify(singles[1]) && JSON.stringify(batch[2]) === JSON.stringify(singles[0]);
+  }
   out.detect = sift.detect(image, { number_of_octaves: P.num_octaves, scales_per_octave: P.scales_per_octave,
     min_blur_level: P.min_blur, assumed_blur: P.assumed_blur }).length;
   // worker protocol (background.js:14-50)
