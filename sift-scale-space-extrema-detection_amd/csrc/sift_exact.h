@@ -10,6 +10,13 @@
 
 namespace sift {
 
+// LDS hand-off between the lanes of one wave: its LDS operations complete in
+// order, so waiting for its own (and a wave barrier) is all the ordering.
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 constexpr int kExactBatch = 16;  // <= kWPad: the zero taps after a weight vector cover a partial batch
 static_assert(kExactBatch <= kWPad, "batched taps stay inside the zero padding");
 
@@ -18,8 +25,9 @@ __host__ __device__ inline int exact_scratch_doubles(int rmax) { return 12 * (2 
 
 // DoG patch d[k][a][c] of image im for DoG scales s-1+k (k = 0..2), rows
 // y-1+a, cols x-1+c, from the L-scales s-1..s+2.  Result in lds d27[27] (visible to all
-// lanes).  Requires blockDim.x == 64 (one wave): __syncthreads() is a wave
-// barrier.  The four L-scales' vertical sums run side by side (one pass over
+// lanes of the calling wave).  One wave per call: the LDS hand-offs are
+// wave-local (wave_sync), so several waves of a block may each work on their
+// own patch with their own sh / Lbuf / d27.  The four L-scales' vertical sums run side by side (one pass over
 // 12 (2r+3) independent fma chains), then 36 lanes form the horizontal sums:
 //   V_t[a][c] = sum_j w_j B(clamp(y-1+a-r+j), clamp(x-1-r+c))
 //   L_t[a][b] = sum_i w_i V_t[a][b + i]            (output column x-1+b)
@@ -35,7 +43,7 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, in
       const double* L0 = P.l64 + im * P.l64_bstride + oc.l64_off + (long long)(s - 1 + k) * plane + (long long)(y - 1 + a) * w + (x - 1 + c);
       d27[lane] = L0[0] - L0[plane];
     }
-    __syncthreads();
+    wave_sync();
     return;
   }
   const int nc0 = 2 * oc.rad[s - 1] + 3, nc1 = 2 * oc.rad[s] + 3, nc2 = 2 * oc.rad[s + 1] + 3,
@@ -64,7 +72,7 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, in
     }
     sh[idx] = acc;
   }
-  __syncthreads();
+  wave_sync();
   if (lane < 36) {
     const int k = lane / 9, q = lane - 9 * k;
     const int a = q / 3, b = q - 3 * a;
@@ -76,12 +84,12 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, in
     for (int i = 0; i <= 2 * r; ++i) acc = fma(wp[i], sh[base + a * nc + b + i], acc);
     Lbuf[lane] = acc;
   }
-  __syncthreads();
+  wave_sync();
   if (lane < 27) {
     const int k = lane / 9, q = lane - 9 * k;
     d27[lane] = Lbuf[9 * k + q] - Lbuf[9 * (k + 1) + q];
   }
-  __syncthreads();
+  wave_sync();
 }
 
 }  // namespace sift

@@ -374,11 +374,12 @@ __global__ __launch_bounds__(64) void k_exact_extrema(const Pyramid P, const Exa
 // ambiguous pixel of the word is then decided exactly, as k_exact_extrema
 // decides one key: a saturated (flat) region makes whole words ambiguous,
 // and one wave then settles 62 pixels instead of one.
-constexpr int kWordPixelMax = 4;  // up to this many ambiguous pixels a word is settled pixel by pixel
+constexpr int kWordPixelMax = 4;  // up to this many ambiguous pixels a word is settled pixel by pixel, one per wave
+constexpr int kWordThreads = 256;  // 4 waves per word: the block's chains spread 4x wider (latency)
 
-__global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const ExactLaunch X) {
+__global__ __launch_bounds__(kWordThreads) void k_exact_words(const Pyramid P, const ExactLaunch X) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const unsigned nwd = min(X.counters[kAmbWords], X.amb_cap);
   const unsigned n = min(*X.n, X.cap);
   const int VS = X.amb_lds_stride;
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const Exact
     const unsigned long long amb = X.ambbitmap[gw], cand = X.bitmap[gw];
     // list slot of the row's first candidate in this word
     unsigned c = 0;
-    for (int q = lane; q < xw; q += 64) c += (unsigned)__popcll(X.bitmap[gw - xw + q]);
+    for (int q = lane; q < xw; q += 64) c += (unsigned)__popcll(X.bitmap[gw - xw + q]);  // (each wave the same)
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
     const unsigned base = X.rowoff[(long long)im * X.rows_per_img + X.row_off[o] + rr] + c;
@@ -438,31 +439,34 @@ __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const Exact
     };
     if (__popcll(amb) <= kWordPixelMax) {
       // a few ambiguous pixels: their 3x3x3 patches alone (wave_dog_patch,
-      // 12 (2r + 3) chains each) cost less than the word's block (12 (64 + 2r))
-      double* d27 = smem;
-      double* Lp = smem + 32;
-      double* sh = smem + 32 + 40;
-      for (unsigned long long m = amb; m; m &= m - 1) {
+      // 12 (2r + 3) chains each) cost less than the word's block (12 (64 +
+      // 2r)); wave w takes the w-th pixel, in its own LDS slice
+      double* d27 = smem + wv * X.amb_patch_stride;
+      double* Lp = d27 + 32;
+      double* sh = d27 + 32 + 40;
+      unsigned long long m = amb;
+      for (int i = 0; i < wv && m; ++i) m &= m - 1;
+      if (m) {
         const int ln = __ffsll((long long)m);  // bit ln - 1 <-> lane ln
         wave_dog_patch(P, im, o, s, y, x0 + ln, sh, Lp, d27);
         if (lane == 0) settle(ln, d27[13], [&](int k, int a, int dc) { return d27[k * 9 + a * 3 + 1 + dc]; });
-        __syncthreads();  // d27 is reused by the next pixel
       }
+      __syncthreads();  // the slices are reused by the next word
       continue;
     }
     if (oc.l64_off >= 0) {
       const long long plane = (long long)h * w;
       const double* L0 = P.l64 + im * P.l64_bstride + oc.l64_off;
-      const int xx = clampi(x0 + lane, 0, w - 1);
-      for (int ta = 0; ta < 12; ++ta) {
+      for (int i = tid; i < 12 * 64; i += kWordThreads) {
+        const int ta = i >> 6, cl = i & 63;
         const int t = s - 1 + ta / 3, a = ta % 3;
-        Lb[ta * 64 + lane] = L0[t * plane + (long long)(y - 1 + a) * w + xx];
+        Lb[i] = L0[t * plane + (long long)(y - 1 + a) * w + clampi(x0 + cl, 0, w - 1)];
       }
     } else {
       for (int t4 = 0; t4 < 4; ++t4) {
         const int t = s - 1 + t4, r = oc.rad[t], nc = 64 + 2 * r;
         const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
-        for (int idx = lane; idx < 3 * nc; idx += 64) {
+        for (int idx = tid; idx < 3 * nc; idx += kWordThreads) {
           const int a = idx / nc, cc = idx - a * nc;
           const int xx = clampi(x0 - r + cc, 0, w - 1);
           const int yb = y - 1 + a - r;
@@ -478,7 +482,7 @@ __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const Exact
         }
       }
       __syncthreads();
-      for (int ta = 0; ta < 12; ++ta) {
+      for (int ta = wv; ta < 12; ta += kWordThreads / 64) {
         const int t = s - 1 + ta / 3, r = oc.rad[t];
         const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[t]);
         const double* vr = V + ta * VS + lane;
@@ -488,7 +492,7 @@ __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const Exact
       }
     }
     __syncthreads();
-    if (lane >= 1 && lane <= kXW && ((amb >> (lane - 1)) & 1ull)) {
+    if (wv == 0 && lane >= 1 && lane <= kXW && ((amb >> (lane - 1)) & 1ull)) {
       auto D = [&](int k, int a, int cl) { return Lb[(k * 3 + a) * 64 + cl] - Lb[((k + 1) * 3 + a) * 64 + cl]; };
       settle(lane, D(1, 1, lane), [&](int k, int a, int dc) { return D(k, a, lane + dc); });
     }
@@ -496,16 +500,18 @@ __global__ __launch_bounds__(64) void k_exact_words(const Pyramid P, const Exact
   }
 }
 
-size_t exact_words_lds_bytes(const Pyramid& P, int* stride) {
+size_t exact_words_lds_bytes(const Pyramid& P, int* stride, int* patch_stride) {
   int rmax = 0;
   for (int o = 0; o < P.O; ++o)
     if (P.oct[o].l64_off < 0) rmax = std::max(rmax, P.oct[o].rmax);
   *stride = 64 + 2 * rmax;
-  return std::max(sizeof(double) * (size_t)(12 * (*stride) + 12 * 64), exact_lds_bytes(P));
+  *patch_stride = (int)(exact_lds_bytes(P) / sizeof(double));  // one wave_dog_patch slice per wave
+  return std::max(sizeof(double) * (size_t)(12 * (*stride) + 12 * 64),
+                  (size_t)(kWordThreads / 64) * exact_lds_bytes(P));
 }
 
 hipError_t launch_exact_words(const Pyramid& P, ExactLaunch X, hipStream_t st) {
-  const size_t lds = exact_words_lds_bytes(P, &X.amb_lds_stride);
+  const size_t lds = exact_words_lds_bytes(P, &X.amb_lds_stride, &X.amb_patch_stride);
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute((const void*)k_exact_words, hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)std::min<size_t>(lds, 160 * 1024));
@@ -513,7 +519,7 @@ hipError_t launch_exact_words(const Pyramid& P, ExactLaunch X, hipStream_t st) {
     if (lds > 160 * 1024) return hipErrorInvalidValue;
   }
   const unsigned grid = std::max(1u, std::min(X.amb_cap, 4096u));
-  hipLaunchKernelGGL(k_exact_words, dim3(grid), dim3(64), lds, st, P, X);
+  hipLaunchKernelGGL(k_exact_words, dim3(grid), dim3(kWordThreads), lds, st, P, X);
   return hipGetLastError();
 }
 

@@ -143,6 +143,7 @@ struct ExactLaunch {
   int rows_per_img;
   const unsigned long long* ambbitmap;  // ambiguous words (k_exact_words; nullptr: amb_keys are pixel keys)
   int amb_lds_stride;            // k_exact_words: doubles per vertical-sum row (64 + 2 rmax)
+  int amb_patch_stride;          // ... doubles per wave of the per-pixel patch scratch
 };
 
 struct RefineLaunch {
