@@ -32,8 +32,15 @@ __device__ __forceinline__ float from_right(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
 }
 
-__device__ __forceinline__ float max3f(float a, float b, float c) { return __builtin_fmaxf(a, __builtin_fmaxf(b, c)); }
-__device__ __forceinline__ float min3f(float a, float b, float c) { return __builtin_fminf(a, __builtin_fminf(b, c)); }
+// IEEE 754-2019 maximum / minimum (v_maximum3_f32 / v_minimum3_f32 on
+// gfx950).  fmaxf / fminf lower to v_max_f32 behind a canonicalising
+// v_max_f32 x, x, x of every loaded or DPP-moved operand (sNaN quieting in
+// IEEE mode): 3 extra VALU per plane row.  The planes hold no NaN, and a
+// -0 / +0 choice cannot change a comparison, so the decisions are the same.
+__device__ __forceinline__ float fmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float fmin2(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmax2(a, fmax2(b, c)); }
+__device__ __forceinline__ float min3f(float a, float b, float c) { return fmin2(a, fmin2(b, c)); }
 
 // Per-wave state of the 3-row window over NP consecutive DoG planes (the
 // centre planes 1..NP-2 are scales, 0 and NP-1 their outer neighbours).
@@ -59,9 +66,9 @@ __device__ __forceinline__ void x_derive(XWin<NP>& Wn, const float (&src)[NP]) {
   for (int q = 0; q < NP; ++q) {
     const float v = src[q];
     const float l = from_left(v), r = from_right(v);
-    const float m2 = __builtin_fmaxf(l, r), n2 = __builtin_fminf(l, r);
-    Wn.hx[K][q] = __builtin_fmaxf(m2, v);
-    Wn.hn[K][q] = __builtin_fminf(n2, v);
+    const float m2 = fmax2(l, r), n2 = fmin2(l, r);
+    Wn.hx[K][q] = fmax2(m2, v);
+    Wn.hn[K][q] = fmin2(n2, v);
     if (q >= 1 && q <= NP - 2) {
       Wn.ex[K][q] = m2;
       Wn.en[K][q] = n2;

@@ -443,10 +443,11 @@ def detect_sharded_device_local(ctx, d_img, params, n_shards, max_overhead=0.5, 
     return out, plan
 
 
-def gather_rows(t, counts, group=None):
-    """all_gather of a ragged first dimension (every rank knows all counts):
-    pad to the largest, all_gather_into_tensor, strip.  Returns the rank-order
-    concatenation."""
+def gather_rows_start(t, counts, group=None):
+    """Start an all_gather of a ragged first dimension (every rank knows all
+    counts): pad to the largest, all_gather_into_tensor with async_op (under
+    nccl it runs on RCCL's own stream, beside later work on the library's
+    stream).  gather_rows_finish waits and strips."""
     import torch
     import torch.distributed as dist
     world = len(counts)
@@ -454,8 +455,31 @@ def gather_rows(t, counts, group=None):
     send = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     send[:t.shape[0]] = t
     recv = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(recv, send, group=group)
-    return torch.cat([recv[i * m:i * m + counts[i]] for i in range(world)])
+    work = dist.all_gather_into_tensor(recv, send, group=group, async_op=True)
+    return work, recv, m, list(counts), send
+
+
+def gather_rows_finish(pending):
+    """The rank-order concatenation of a gather_rows_start."""
+    import torch
+    work, recv, m, counts, _send = pending
+    work.wait()
+    return torch.cat([recv[i * m:i * m + counts[i]] for i in range(len(counts))])
+
+
+def gather_rows(t, counts, group=None):
+    """all_gather of a ragged first dimension: the rank-order concatenation."""
+    return gather_rows_finish(gather_rows_start(t, counts, group))
+
+
+def _gather_counts(cnt, world, group, dev):
+    """Every rank's per-(octave, scale) block counts (int64 [world, O*S] host)."""
+    import torch
+    import torch.distributed as dist
+    mine = torch.from_numpy(np.asarray(cnt, dtype=np.int64)).to(dev)
+    out = torch.zeros(world * mine.numel(), dtype=torch.int64, device=mine.device)
+    dist.all_gather_into_tensor(out, mine, group=group)
+    return out.view(world, -1).cpu().numpy()
 
 
 def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, timer=None):
@@ -481,27 +505,36 @@ def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, time
     else:
         kp, cnt, seed = torch.zeros((0, REC), dtype=torch.uint8, device=dev), np.zeros(0, np.int64), None
     t0 = _tick(timer, "band", t0)
-    kps, cnts = [kp], [_blocks(cnt, O, S)]
-    if plan.has_tail:
-        cols = octave_dims(W, H, plan.num_octaves)[plan.K + 1][1]
-        rows = [(lambda a: a[1] - a[0])(_seed_rows(plan, r)) if r < nb else 0 for r in range(world)]
-        mine = seed if seed is not None else torch.zeros((0, cols), dtype=torch.float64, device=dev)
-        base = gather_rows(mine, rows, group)
-        t0 = _tick(timer, "base_gather", t0)
-        for t, owner in sorted(tail_octaves(plan, world).items()):  # a rank's list stays in block order
-            if owner == rank:
-                tk, tc = run_tail_octave_device(ctx, base, params, plan, t)
-                kps.append(tk)
-                cnts.append(_blocks(tc, O, S))
-        t0 = _tick(timer, "tail", t0)
-    kp = torch.cat(kps)
-    mine_cnt = torch.from_numpy(np.sum(cnts, axis=0).astype(np.int64)).to(dev)
-    all_cnt = torch.zeros(world * O * S, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(all_cnt, mine_cnt, group=group)
-    counts = all_cnt.view(world, O * S).cpu().numpy()
-    all_kp = gather_rows(kp, [int(c) for c in counts.sum(axis=1)], group)
+    # The band keypoints' all-gather starts as soon as the bands are done and
+    # runs on RCCL's stream while the tail octaves run on the library's; only
+    # the (few) tail keypoints are gathered after the tail.  The merge takes
+    # the band parts, then the tail parts: no block holds both (the tail
+    # octaves are K+1..O-1), so block-major-then-part order is unchanged.
+    band_counts = _gather_counts(_blocks(cnt, O, S), world, group, dev)
+    band = gather_rows_start(kp, [int(c) for c in band_counts.sum(axis=1)], group)
+    if not plan.has_tail:
+        all_kp = gather_rows_finish(band)
+        t0 = _tick(timer, "kp_gather", t0)
+        out = _merge_gathered(ctx, all_kp, band_counts, O, S)
+        _tick(timer, "merge", t0)
+        return out, plan
+    cols = octave_dims(W, H, plan.num_octaves)[plan.K + 1][1]
+    rows = [(lambda a: a[1] - a[0])(_seed_rows(plan, r)) if r < nb else 0 for r in range(world)]
+    mine = seed if seed is not None else torch.zeros((0, cols), dtype=torch.float64, device=dev)
+    base = gather_rows(mine, rows, group)
+    t0 = _tick(timer, "base_gather", t0)
+    tkps, tcnts = [torch.zeros((0, REC), dtype=torch.uint8, device=dev)], [np.zeros(O * S, np.int64)]
+    for t, owner in sorted(tail_octaves(plan, world).items()):  # a rank's list stays in block order
+        if owner == rank:
+            tk, tc = run_tail_octave_device(ctx, base, params, plan, t)
+            tkps.append(tk)
+            tcnts.append(_blocks(tc, O, S))
+    t0 = _tick(timer, "tail", t0)
+    tail_counts = _gather_counts(np.sum(tcnts, axis=0), world, group, dev)
+    tail_kp = gather_rows(torch.cat(tkps), [int(c) for c in tail_counts.sum(axis=1)], group)
+    all_kp = torch.cat([gather_rows_finish(band), tail_kp])
     t0 = _tick(timer, "kp_gather", t0)
-    out = _merge_gathered(ctx, all_kp, counts, O, S)
+    out = _merge_gathered(ctx, all_kp, np.concatenate([band_counts, tail_counts]), O, S)
     _tick(timer, "merge", t0)
     return out, plan
 

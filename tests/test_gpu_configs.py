@@ -30,6 +30,10 @@ from sift_amd.synth import blob_image
 pytestmark = pytest.mark.gpu
 
 
+def ctx_octaves(p):
+    return p.num_octaves
+
+
 def _vs_oracle(ctx, img, p, mode, low_rtol=0.0):
     """low_rtol == 0: the low-contrast list (F_LOW_CONTRAST_LIST) must equal
     the oracle's too (positions exact, values within fp32 rounding)."""
@@ -56,8 +60,18 @@ def _vs_oracle(ctx, img, p, mode, low_rtol=0.0):
             float(np.abs(kp["interp_value"] - r.refined[:, 7]).max(initial=0.0))))
     check_candidates(cand, r.candidates())
     check_keypoints(kp, r.refined)
-    assert abs(counts["low_contrast"] - r.n_low) <= low_rtol * r.n_low, (counts["low_contrast"], r.n_low)
     assert low.shape[0] == counts["low_contrast"]
+    if low_rtol > 0.0:  # report the low-contrast set difference (positions)
+        def pos(a):
+            return set(map(tuple, np.asarray(a).tolist()))
+        g = pos(np.stack([low["octave"], low["scale"], low["x"], low["y"]], 1))
+        rl = r.low_contrast()
+        o_ = pos(rl[:, :4].astype(np.int64))
+        print("low-contrast: GPU %d, oracle %d, only GPU %d, only oracle %d (per octave %s / %s)" % (
+            len(g), len(o_), len(g - o_), len(o_ - g),
+            np.bincount([t[0] for t in g - o_], minlength=ctx_octaves(p)).tolist(),
+            np.bincount([t[0] for t in o_ - g], minlength=ctx_octaves(p)).tolist()))
+    assert abs(counts["low_contrast"] - r.n_low) <= low_rtol * r.n_low, (counts["low_contrast"], r.n_low)
     if low_rtol == 0.0:
         check_candidates(low, r.low_contrast())
     assert counts["singular"] == r.n_singular == 0
@@ -112,15 +126,17 @@ def test_cfg5_8k_o6_s5_whole_vs_8_row_band_shards(gpu_ctx, img8k):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("mode", [orc.CONV_SEPARABLE, orc.CONV_SEPARABLE_FMA_VH], ids=["separable", "gpu_order"])
+@pytest.mark.parametrize("mode", [orc.CONV_SEPARABLE, orc.CONV_SEPARABLE_FMA_VH, orc.CONV_2D],
+                         ids=["separable", "gpu_order", "reference_2d"])
 def test_cfg5_8k_o6_s5_matches_oracle(gpu_ctx, img8k, mode):
     """The whole 8K image against the oracle.  Candidates and keypoints must
-    be identical in both summation orders.  The low-contrast count is exact
-    against the oracle in the HIP path's own operation order (columns then
-    rows, fma chains); against the rows-first order it may differ by a few of
-    ~435 K: low-contrast extrema in flat regions whose 26 neighbours tie to
-    the last fp64 bit, which either summation order may break (the reference's
-    2D order is a third one; 4K matches it exactly, above)."""
+    be identical in all three summation orders, the reference's own 2D-kernel
+    order (sift.js:96-128) included.  The low-contrast list is exact against
+    the oracle in the HIP path's own operation order (columns then rows, fma
+    chains); against the rows-first and the 2D order its count may differ by
+    a few of ~435 K -- low-contrast extrema in flat regions whose 26
+    neighbours tie to the last fp64 bit, which each summation order breaks its
+    own way -- and the test prints the set difference per octave."""
     kp, _ = _vs_oracle(gpu_ctx, img8k, sift_amd.make_params(6, 5), mode,
                        low_rtol=0.0 if mode == orc.CONV_SEPARABLE_FMA_VH else 1e-5)
     assert kp.shape[0] > 1000000

@@ -62,7 +62,6 @@ os.environ.setdefault("MASTER_PORT", "29533")
 dist.init_process_group("nccl", rank=0, world_size=1)
 seed_rows = [(lambda a: a[1] - a[0])(shard._seed_rows(plan, r)) for r in range(len(plan.bands))]
 cols = sift_amd.octave_dims(W, H, O)[plan.K + 1][1]
-n_kp_total = n_whole
 
 
 def t_gather(nbytes_per_rank, world):
@@ -81,12 +80,26 @@ def t_gather(nbytes_per_rank, world):
     return local, model
 
 
+# Keypoints per rank: a band's (octaves 0..K, its own rows; abs_y decides the
+# band here, a model) and a tail owner's (its octaves > K).
+kpa = np.frombuffer(whole, dtype=sift_amd.KEYPOINT_DTYPE)
+band_n = [int(((kpa["octave"] <= plan.K) & (kpa["abs_y"] >= lo) & (kpa["abs_y"] < hi)).sum())
+          for lo, hi in plan.bands]
+tail_n = [0] * len(plan.bands)
+for t, r in owner.items():
+    tail_n[r] += int((kpa["octave"] == t).sum())
 base_pad = max(seed_rows) * cols * 8
-kp_pad = int(np.ceil(n_kp_total / len(plan.bands) * 1.15)) * 48  # parts are padded to the largest (+15 % spread)
+kp_pad = max(band_n) * 48   # parts are padded to the largest
+tkp_pad = max(max(tail_n), 1) * 48
 base_local, base_model = t_gather(base_pad, n)
 kp_local, kp_model = t_gather(kp_pad, n)
+tkp_local, tkp_model = t_gather(tkp_pad, n)
 dist.destroy_process_group()
-crit = max(shards) + base_model + max(tails.values() or [0.0]) + kp_model + med["merge"]
+# The band keypoints' all-gather runs during the tail octaves (shard.detect_sharded_device);
+# after the tail only the tail keypoints are gathered.
+tail_max = max(tails.values() or [0.0])
+crit = max(shards) + base_model + max(tail_max + tkp_model, kp_model) + med["merge"]
+crit_serial = max(shards) + base_model + tail_max + kp_model + tkp_model + med["merge"]
 print(json.dumps({"config": "8K 7680x4320 O6 S5, device-resident (image in HBM, keypoints in HBM)",
                   "n_shards": n, "K": plan.K, "bands": plan.bands, "crops": plan.crops,
                   "whole_ms": round(1e3 * float(np.median(t_whole)), 3),
@@ -97,12 +110,17 @@ print(json.dumps({"config": "8K 7680x4320 O6 S5, device-resident (image in HBM, 
                   "merge_ms": round(med["merge"], 3),
                   "base_gather": {"bytes_per_rank": base_pad, "nccl_world1_ms": round(base_local, 3),
                                   "model_ms": round(base_model, 3)},
+                  "band_keypoints_per_rank": band_n, "tail_keypoints_per_rank": tail_n,
                   "kp_gather": {"bytes_per_rank": kp_pad, "nccl_world1_ms": round(kp_local, 3),
                                 "model_ms": round(kp_model, 3)},
+                  "tail_kp_gather": {"bytes_per_rank": tkp_pad, "nccl_world1_ms": round(tkp_local, 3),
+                                     "model_ms": round(tkp_model, 3)},
                   "xgmi_GBps_model": xgmi,
                   "critical_path_ms": round(crit, 3),
-                  "critical_path_note": "phases are sequential (every tail octave starts from the gathered base): "
-                                        "slowest band + base all-gather (model) + slowest tail octave + keypoint "
-                                        "all-gather (model) + block merge",
+                  "critical_path_serial_gathers_ms": round(crit_serial, 3),
+                  "critical_path_note": "every tail octave starts from the gathered base: slowest band + base "
+                                        "all-gather (model) + max(slowest tail octave + tail-keypoint all-gather, "
+                                        "band-keypoint all-gather running beside the tail) (models) + concatenation "
+                                        "and block merge",
                   "speedup_vs_whole": round(1e3 * float(np.median(t_whole)) / crit, 2),
                   "keypoints": n_whole, "identical": bool(same)}))
