@@ -340,9 +340,12 @@ int sift_detect_from_seed_device(struct sift_ctx *ctx, int octave_first, const d
 /* Detection of a tail of octaves split over several devices (ABI version >= 5):
  * like sift_detect_from_seed_device, building octaves octave_first ..
  * p->num_octaves - 1 from the fp64 base of octave_first, but scanning only
- * octaves octave_scan_first .. p->num_octaves - 1 for extrema (the octaves
- * before it are built for their seeds only).  Rank j of a row-band run builds
- * the tail up to its octave and detects that one octave. */
+ * octaves octave_scan_first .. p->num_octaves - 1 for extrema.  The octaves
+ * before it are evaluated for their successor's base only (L[S] at even rows
+ * and columns, bit-identical to the full build): they have no Gaussian or
+ * DoG planes (sift_get_plane returns SIFT_E_STATE for them).  Rank j of a
+ * row-band run builds the tail up to its octave and detects that one
+ * octave. */
 int sift_detect_from_seed_range_device(struct sift_ctx *ctx, int octave_first, int octave_scan_first,
                                        const double *d_seed, int width, int height, const sift_params *p,
                                        sift_keypoint *out, size_t cap, size_t *n_out);
@@ -352,7 +355,9 @@ int sift_detect_from_seed_range_device(struct sift_ctx *ctx, int octave_first, i
  * counts[q * n_blocks + b] keypoints of block b.  d_out receives block 0 of
  * every list in list order, then block 1, ...  With blocks = (octave, scale)
  * and lists = row bands in row order, this is the reference's candidate order
- * (octave, scale, y, x) without a sort.  counts is host memory; completes
+ * (octave, scale, y, x) without a sort.  A negative count skips that many
+ * records of list q in d_in (padding, e.g. of an all-gather padded to the
+ * largest list); they are not copied.  counts is host memory; completes
  * before return. */
 int sift_merge_keypoint_blocks_device(struct sift_ctx *ctx, const sift_keypoint *d_in, const int64_t *counts,
                                       int n_parts, int n_blocks, sift_keypoint *d_out);

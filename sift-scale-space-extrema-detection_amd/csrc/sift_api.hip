@@ -88,6 +88,7 @@ struct sift_ctx {
   ExtremaLaunch xl{};       // extrema launch state between prepare / scan / finish
   int o_first = 0;          // first octave of the pyramid in use (sift_detect_from_seed: > 0)
   int scan_first = 0;       // first octave the extrema stage scans (>= o_first; sift_detect_from_seed_range)
+  int planes_first = 0;     // first octave with Gaussian / DoG planes (below: only its successor's base)
   int row0 = 0;             // sift_set_row_origin: input row of the image's first row
   int xseed_h = 0, xseed_w = 0;  // SIFT_F_EXPORT_NEXT_SEED: the base of octave O
   bool has_xseed = false;
@@ -102,6 +103,7 @@ struct sift_ctx {
   DBuf base0;                                  // materialised octave-0 base (large radii only)
   DBuf l64;                                    // fp64 Gaussian planes of the large-radius octaves
   DBuf vsplit;                                 // vertical-sum scratch of the split-pass octaves (one at a time)
+  DBuf seedv;                                  // vertical sums of the seed-only octaves (launch_seed_only)
   long long vsplit_pi = 0;                     // ... doubles per image of a batch
   std::vector<double> wts_host;                // taps last uploaded to wts
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
@@ -278,6 +280,7 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
   const int O = p->num_octaves, S = p->scales_per_octave, NS = S + 3, ND = S + 2;
   ctx->p = *p;
   ctx->scan_first = 0;
+  ctx->planes_first = 0;
   ctx->W = W;
   ctx->H = H;
   ctx->dims.assign(2 * O, 0);
@@ -389,7 +392,7 @@ static bool fuse_enabled(const sift_params* p) {
 static int build_common(sift_ctx* ctx, const float* img_host, const float* img_dev, int W, int H,
                         size_t stride, const sift_params* p, const double* sig,
                         int o_first = 0, const double* seed_host = nullptr, const double* seed_dev = nullptr,
-                        bool fuse_extrema = false, int nimg = 1, size_t img_bstride = 0) {
+                        bool fuse_extrema = false, int nimg = 1, size_t img_bstride = 0, int seed_only_below = 0) {
   if (!ctx) return SIFT_E_ARG;
   if (o_first == 0 && !img_host && !img_dev) return set_err(ctx, SIFT_E_ARG, "null image");
   if (o_first > 0 && !seed_host && !seed_dev) return set_err(ctx, SIFT_E_ARG, "null seed");
@@ -401,6 +404,12 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   if (o_first < 0 || o_first >= P.O) return set_err(ctx, SIFT_E_ARG, "octave_first out of range");
   ctx->o_first = o_first;
   ctx->scan_first = o_first;
+  // Octaves [o_first, so_end) only feed their successor's base (a range
+  // detection scans from so_end): launch_seed_only, no planes.
+  const int so_end = std::min(std::max(o_first, seed_only_below), P.O - 1);
+  if (so_end > o_first && (nimg > 1 || fuse_extrema))
+    return set_err(ctx, SIFT_E_UNSUPPORTED, "seed-only octaves: single image, no fused decisions");
+  ctx->planes_first = so_end;
   ctx->has_xseed = false;
   const long long tot = total_plane_px(ctx);
   const bool keep_gauss = !(p->flags & SIFT_F_SKIP_GAUSS_PLANES);
@@ -445,7 +454,7 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   P.dog = ctx->dog.as<float>();
   {  // large-radius octaves keep their fp64 Gaussian planes (the exact passes read them)
     long long l64 = 0;
-    for (int o = o_first; o < P.O; ++o)
+    for (int o = so_end; o < P.O; ++o)
       if (gauss_keep_l64(P, o)) {
         P.oct[o].l64_off = l64;
         l64 += (long long)P.NS * P.oct[o].h * P.oct[o].w;
@@ -454,8 +463,11 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     P.l64 = l64 ? ctx->l64.as<double>() : nullptr;
     P.l64_bstride = l64;
     size_t vs = 0;  // the split-pass octaves run in turn on this stream: one scratch (per image)
-    for (int o = o_first; o < P.O; ++o)
+    for (int o = so_end; o < P.O; ++o)
       if (gauss_vsplit(P, o)) vs = std::max(vs, (size_t)P.NS * P.oct[o].h * P.oct[o].w);
+    size_t sv = 0;
+    for (int o = o_first; o < so_end; ++o) sv = std::max(sv, seed_only_scratch(P, o));
+    if (sv) HIPCHK(ctx->seedv.ensure(sv * sizeof(double)));
     if (vs) HIPCHK(ctx->vsplit.ensure(vs * nimg * sizeof(double)));
     ctx->vsplit_pi = (long long)vs;
   }
@@ -483,6 +495,13 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   }
   for (int o = o_first; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
+    if (o < so_end) {
+      HIPCHK(launch_seed_only(P, o, ctx->seeds.as<double>() + oc.seed_off, ctx->seedv.as<double>(),
+                              ctx->seeds.as<double>() + P.oct[o + 1].seed_off, ctx->stream));
+      if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
+      HIPCHK(hipEventRecord(ctx->ev_go[o], ctx->stream));
+      continue;
+    }
     GaussLaunch L{};
     L.o = o;
     L.base = o == 0 ? base0 : ctx->seeds.as<double>() + oc.seed_off;
@@ -586,7 +605,7 @@ int sift_get_plane(sift_ctx* ctx, int kind, int o, int s, float* dst, size_t cap
   if (ctx->dog_source == kNone) return set_err(ctx, SIFT_E_STATE, "no pyramid");
   const Pyramid& P = ctx->P;
   if (o < 0 || o >= P.O) return set_err(ctx, SIFT_E_ARG, "octave out of range");
-  if (o < ctx->o_first) return set_err(ctx, SIFT_E_STATE, "octave not built (sift_detect_from_seed)");
+  if (o < ctx->planes_first) return set_err(ctx, SIFT_E_STATE, "octave not built (sift_detect_from_seed[_range])");
   const Octave& oc = P.oct[o];
   const size_t plane = (size_t)oc.h * oc.w;
   if (cap_px < plane) return set_err(ctx, SIFT_E_CAPACITY, "destination too small");
@@ -622,6 +641,7 @@ int sift_load_dog(sift_ctx* ctx, const float* planes, int width, int height, con
   ctx->dog_source = kForeign;
   ctx->o_first = 0;
   ctx->scan_first = 0;
+  ctx->planes_first = 0;
   ctx->have_gauss = false;
   ctx->have_cand = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -651,6 +671,7 @@ int sift_load_scale_space(sift_ctx* ctx, const float* planes, int width, int hei
   ctx->dog_source = kForeign;
   ctx->o_first = 0;
   ctx->scan_first = 0;
+  ctx->planes_first = 0;
   ctx->have_gauss = true;
   ctx->have_cand = false;
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1529,7 +1550,8 @@ static int detect_from_seed(sift_ctx* ctx, int o_first, const double* seed_host,
   if (o_first < 1) return set_err(ctx, SIFT_E_ARG, "octave_first must be >= 1");
   if (scan_first && (scan_first < o_first || scan_first >= p->num_octaves))
     return set_err(ctx, SIFT_E_ARG, "octave_scan_first outside [octave_first, num_octaves)");
-  int rc = build_common(ctx, nullptr, nullptr, W, H, 0, p, nullptr, o_first, seed_host, seed_dev);
+  int rc = build_common(ctx, nullptr, nullptr, W, H, 0, p, nullptr, o_first, seed_host, seed_dev, false, 1, 0,
+                        scan_first);
   if (rc) return rc;
   if (scan_first) ctx->scan_first = scan_first;
   rc = launch_extrema_stage(ctx);
@@ -1570,8 +1592,7 @@ int sift_merge_keypoint_blocks_device(sift_ctx* ctx, const sift_keypoint* d_in, 
     long long a = 0;
     for (int b = 0; b < nb; ++b) {
       const long long c = counts[(size_t)q * nb + b];
-      if (c < 0) return set_err(ctx, SIFT_E_ARG, "negative count");
-      a += c;
+      a += c < 0 ? -c : c;  // negative: skipped records (padding)
     }
     part_start[q + 1] = part_start[q] + a;
   }
@@ -1581,7 +1602,10 @@ int sift_merge_keypoint_blocks_device(sift_ctx* ctx, const sift_keypoint* d_in, 
   for (int b = 0; b < nb; ++b)
     for (int q = 0; q < np; ++q) {
       const long long c = counts[(size_t)q * nb + b];
-      if (!c) continue;
+      if (c <= 0) {
+        in_at[q] -= c;
+        continue;
+      }
       seg.push_back(in_at[q] * kRec);
       seg.push_back(o * kRec);
       seg.push_back(c * kRec);
@@ -1688,7 +1712,7 @@ static int plane_image_common(sift_ctx* ctx, int kind, int o, int s, int mode, d
   if (mode < SIFT_DISPLAY_PLAIN || mode > SIFT_DISPLAY_SAMPLED) return set_err(ctx, SIFT_E_ARG, "bad display mode");
   const Pyramid& P = ctx->P;
   if (o < 0 || o >= P.O) return set_err(ctx, SIFT_E_ARG, "octave out of range");
-  if (o < ctx->o_first) return set_err(ctx, SIFT_E_STATE, "octave not built (sift_detect_from_seed)");
+  if (o < ctx->planes_first) return set_err(ctx, SIFT_E_STATE, "octave not built (sift_detect_from_seed[_range])");
   const Octave& oc = P.oct[o];
   const size_t plane = (size_t)oc.h * oc.w;
   if (cap_bytes < plane * 4) return set_err(ctx, SIFT_E_CAPACITY, "destination too small (4 bytes per pixel)");

@@ -31,11 +31,20 @@ __host__ __device__ inline int exact_scratch_doubles(int rmax) { return 12 * (2 
 // 12 (2r+3) independent fma chains), then 36 lanes form the horizontal sums:
 //   V_t[a][c] = sum_j w_j B(clamp(y-1+a-r+j), clamp(x-1-r+c))
 //   L_t[a][b] = sum_i w_i V_t[a][b + i]            (output column x-1+b)
-__device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, int y, int x, double* sh,
-                                      double* Lbuf /*36*/, double* d27) {
+// NT = 64: one wave per patch (wave-local hand-offs).  NT > 64: the NT
+// threads of a block share one patch (its vertical chains spread NT wide:
+// at radius 47 a wave's lanes walk ~15 chains of 95 dependent loads each,
+// the latency of the exact refinement; block barriers for the hand-offs).
+template <int NT>
+__device__ inline void dog_patch(const Pyramid& P, int im, int o, int s, int y, int x, double* sh,
+                                 double* Lbuf /*36*/, double* d27) {
   const Octave& oc = P.oct[o];
   const int h = oc.h, w = oc.w;
-  const int lane = threadIdx.x & 63;
+  const int lane = NT == 64 ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  auto wave_sync = [] {
+    if (NT == 64) sift::wave_sync();
+    else __syncthreads();
+  };
   if (oc.l64_off >= 0) {  // the wide-radius path kept this octave's fp64 Gaussian planes: the values themselves
     if (lane < 27) {
       const int k = lane / 9, q = lane - 9 * k, a = q / 3, c = q - 3 * a;
@@ -49,7 +58,7 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, in
   const int nc0 = 2 * oc.rad[s - 1] + 3, nc1 = 2 * oc.rad[s] + 3, nc2 = 2 * oc.rad[s + 1] + 3,
             nc3 = 2 * oc.rad[s + 2] + 3;
   const int o1 = 3 * nc0, o2 = o1 + 3 * nc1, o3 = o2 + 3 * nc2, o4 = o3 + 3 * nc3;
-  for (int idx = lane; idx < o4; idx += 64) {
+  for (int idx = lane; idx < o4; idx += NT) {
     const int k = idx >= o3 ? 3 : idx >= o2 ? 2 : idx >= o1 ? 1 : 0;
     const int base = k == 3 ? o3 : k == 2 ? o2 : k == 1 ? o1 : 0;
     const int nc = k == 3 ? nc3 : k == 2 ? nc2 : k == 1 ? nc1 : nc0;
@@ -90,6 +99,11 @@ __device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, in
     d27[lane] = Lbuf[9 * k + q] - Lbuf[9 * (k + 1) + q];
   }
   wave_sync();
+}
+
+__device__ inline void wave_dog_patch(const Pyramid& P, int im, int o, int s, int y, int x, double* sh,
+                                      double* Lbuf /*36*/, double* d27) {
+  dog_patch<64>(P, im, o, s, y, x, sh, Lbuf, d27);
 }
 
 }  // namespace sift

@@ -1887,6 +1887,57 @@ static size_t lds_path_bytes(const Pyramid& P, int o) {
   return b <= 160 * 1024 ? b : 0;
 }
 
+// The base of octave o+1 alone (sift_detect_from_seed_range_device: an
+// octave below the scanned one only feeds its successor).  background.js:
+// 114-118 samples L_o[S] at even rows and columns, so only those values are
+// evaluated, with the tile kernels' fma chains (vertical then horizontal,
+// taps in increasing order, from 0.0; the oracle's CONV_SEPARABLE_FMA_VH):
+// k_seed_vert forms the vertical sums of the even rows (every column),
+// k_seed_horz the horizontal sums at the even columns.  3/8 of one scale's
+// work instead of all S+3 scales with their planes.
+__global__ __launch_bounds__(256) void k_seed_vert(const Pyramid P, int o, const double* __restrict__ base,
+                                                   double* __restrict__ vrow) {
+  const Octave& oc = P.oct[o];
+  const int x = blockIdx.x * 256 + threadIdx.x, yp = blockIdx.y;
+  if (x >= oc.w) return;
+  const int r = oc.rad[P.S], h = oc.h;
+  const double* __restrict__ wt = P.wts + oc.wofs[P.S];
+  const double* __restrict__ col = base + x;
+  const long long w = oc.w;
+  double acc = 0.0;
+  for (int j = 0; j <= 2 * r; ++j) acc = __builtin_fma(wt[j], col[clampi(2 * yp + j - r, 0, h - 1) * w], acc);
+  vrow[(long long)yp * w + x] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_seed_horz(const Pyramid P, int o, const double* __restrict__ vrow,
+                                                   double* __restrict__ next) {
+  const Octave& oc = P.oct[o];
+  const int nw = P.oct[o + 1].w;
+  const int xp = blockIdx.x * 256 + threadIdx.x, yp = blockIdx.y;
+  if (xp >= nw) return;
+  const int r = oc.rad[P.S], w = oc.w;
+  const double* __restrict__ wt = P.wts + oc.wofs[P.S];
+  const double* __restrict__ row = vrow + (long long)yp * w;
+  double acc = 0.0;
+  for (int i = 0; i <= 2 * r; ++i) acc = __builtin_fma(wt[i], row[clampi(2 * xp + i - r, 0, w - 1)], acc);
+  next[(long long)yp * nw + xp] = acc;
+}
+
+size_t seed_only_scratch(const Pyramid& P, int o) {
+  return (size_t)P.oct[o + 1].h * P.oct[o].w;
+}
+
+hipError_t launch_seed_only(const Pyramid& P, int o, const double* base, double* vrow, double* next,
+                            hipStream_t st) {
+  if (o < 0 || o + 1 >= P.O || !base || !vrow || !next) return hipErrorInvalidValue;
+  const Octave& oc = P.oct[o];
+  const Octave& on = P.oct[o + 1];
+  if (2 * (on.h - 1) > oc.h - 1 || 2 * (on.w - 1) > oc.w - 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_seed_vert, dim3((oc.w + 255) / 256, on.h), dim3(256), 0, st, P, o, base, vrow);
+  hipLaunchKernelGGL(k_seed_horz, dim3((on.w + 255) / 256, on.h), dim3(256), 0, st, P, o, vrow, next);
+  return hipGetLastError();
+}
+
 hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st) {
   const long long n = (long long)P.oct[0].h * P.oct[0].w;
   const int blocks = (int)std::min<long long>((n + 255) / 256, 8192);

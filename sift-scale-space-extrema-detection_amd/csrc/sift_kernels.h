@@ -206,6 +206,10 @@ bool gauss_can_fuse(const Pyramid& P, int o);
 // of the input (4 H W doubles) instead of the staged input region.
 bool gauss_needs_base0(const Pyramid& P);
 hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st);
+// The base of octave o+1 from octave o's base alone (no planes): L_o[S] at
+// even rows / columns; vrow: seed_only_scratch(P, o) doubles.
+size_t seed_only_scratch(const Pyramid& P, int o);
+hipError_t launch_seed_only(const Pyramid& P, int o, const double* base, double* vrow, double* next, hipStream_t st);
 // ty_end >= 0: only tile rows [ty_begin, ty_end) of the octave (a band;
 // not for fused or split-pass octaves).
 hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin = 0, int ty_end = -1);

@@ -427,6 +427,7 @@ def detect_sharded_device_local(ctx, d_img, params, n_shards, max_overhead=0.5, 
         kps.append(kp)
         counts.append(cnt)
         seeds.append(seed)
+    tkps, tcounts = [], []
     if plan.has_tail:
         base = torch.cat(seeds)
         for t in sorted(tail_octaves(plan, len(plan.bands))):
@@ -434,13 +435,49 @@ def detect_sharded_device_local(ctx, d_img, params, n_shards, max_overhead=0.5, 
             kp, cnt = run_tail_octave_device(ctx, base, params, plan, t)
             _sync(d_img)
             _tick(timer, "tail%d" % t, t0)
-            kps.append(kp)
-            counts.append(cnt)
+            tkps.append(kp)
+            tcounts.append(cnt)
+    # The parts laid out as the all-gathers leave them (padded to the largest
+    # part), then the distributed driver's merge: bands, then tail octaves.
+    band = _pad_parts(kps, d_img.device)
+    tail = _pad_parts(tkps, d_img.device) if tkps else None
+    nb = int(sum(int(np.sum(c)) for c in counts))
+    nt = int(sum(int(np.sum(c)) for c in tcounts))
+    out = torch.empty((nb + nt, REC), dtype=torch.uint8, device=d_img.device)
+    _sync(d_img)
     t0 = time.perf_counter()
-    out = merge_device(ctx, kps, counts, O, S)
+    _merge_padded(ctx, band[0], band[1], np.stack([_blocks(c, O, S) for c in counts]), out[:nb])
+    if tail is not None:
+        _merge_padded(ctx, tail[0], tail[1], np.stack([_blocks(c, O, S) for c in tcounts]), out[nb:])
     _sync(d_img)
     _tick(timer, "merge", t0)
     return out, plan
+
+
+def _pad_parts(parts, dev):
+    """Parts laid out back to back at the stride of the largest (the layout
+    gather_rows_start's all-gather leaves), as (buffer, stride)."""
+    import torch
+    m = max(max(p.shape[0] for p in parts), 1)
+    buf = torch.zeros((len(parts) * m, REC), dtype=torch.uint8, device=dev)
+    for i, p in enumerate(parts):
+        buf[i * m:i * m + p.shape[0]] = p
+    return buf, m
+
+
+def _merge_padded(ctx, buf, m, blocks, out):
+    """Block-major merge of parts stored at stride m in buf (blocks: int64
+    [parts, O*S] per-part block counts) into out: each part's padding is a
+    trailing negative count, skipped by the merge (no strip copy)."""
+    blocks = np.asarray(blocks, dtype=np.int64)
+    n = blocks.sum(axis=1)
+    if int(n.sum()) == 0:
+        return
+    ext = np.zeros((blocks.shape[0], blocks.shape[1] + 1), dtype=np.int64)
+    ext[:, :-1] = blocks
+    ext[:, -1] = -(m - n)
+    torch_ready(buf)
+    ctx.merge_keypoint_blocks_device(buf.data_ptr(), ext, out.data_ptr())
 
 
 def gather_rows_start(t, counts, group=None):
@@ -512,10 +549,12 @@ def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, time
     # octaves are K+1..O-1), so block-major-then-part order is unchanged.
     band_counts = _gather_counts(_blocks(cnt, O, S), world, group, dev)
     band = gather_rows_start(kp, [int(c) for c in band_counts.sum(axis=1)], group)
+    nb_kp = int(band_counts.sum())
     if not plan.has_tail:
-        all_kp = gather_rows_finish(band)
+        band[0].wait()
         t0 = _tick(timer, "kp_gather", t0)
-        out = _merge_gathered(ctx, all_kp, band_counts, O, S)
+        out = torch.empty((nb_kp, REC), dtype=torch.uint8, device=dev)
+        _merge_padded(ctx, band[1], band[2], band_counts, out)
         _tick(timer, "merge", t0)
         return out, plan
     cols = octave_dims(W, H, plan.num_octaves)[plan.K + 1][1]
@@ -531,19 +570,15 @@ def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, time
             tcnts.append(_blocks(tc, O, S))
     t0 = _tick(timer, "tail", t0)
     tail_counts = _gather_counts(np.sum(tcnts, axis=0), world, group, dev)
-    tail_kp = gather_rows(torch.cat(tkps), [int(c) for c in tail_counts.sum(axis=1)], group)
-    all_kp = torch.cat([gather_rows_finish(band), tail_kp])
+    tail = gather_rows_start(torch.cat(tkps), [int(c) for c in tail_counts.sum(axis=1)], group)
+    tail[0].wait()
+    band[0].wait()
     t0 = _tick(timer, "kp_gather", t0)
-    out = _merge_gathered(ctx, all_kp, np.concatenate([band_counts, tail_counts]), O, S)
+    # The gathered lists stay padded (a trailing negative count per rank skips
+    # the padding); the band blocks (octaves 0..K) precede the tail blocks
+    # (octaves K+1..O-1) in block order, so the two merges fill out in turn.
+    out = torch.empty((nb_kp + int(tail_counts.sum()), REC), dtype=torch.uint8, device=dev)
+    _merge_padded(ctx, band[1], band[2], band_counts, out[:nb_kp])
+    _merge_padded(ctx, tail[1], tail[2], tail_counts, out[nb_kp:])
     _tick(timer, "merge", t0)
     return out, plan
-
-
-def _merge_gathered(ctx, all_kp, counts, O, S):
-    """Merge of the rank-order concatenation of every rank's block-ordered list."""
-    import torch
-    out = torch.empty_like(all_kp)
-    if all_kp.shape[0]:
-        torch_ready(all_kp)
-        ctx.merge_keypoint_blocks_device(all_kp.data_ptr(), counts, out.data_ptr())
-    return out

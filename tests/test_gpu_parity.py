@@ -457,6 +457,37 @@ def test_owned_rows_and_block_counts(gpu_ctx):
         np.testing.assert_array_equal(counts, np.bincount(org[keep, 0] * S + org[keep, 1] - 1, minlength=O * S))
 
 
+@pytest.mark.parametrize("t", [3, 5])
+def test_range_detection_seed_only_octaves_bit_identical(gpu_ctx, t):
+    """sift_detect_from_seed_range_device evaluates the octaves below its scan
+    octave for their successor's base only (launch_seed_only: L[S] at even
+    rows and columns).  The scanned octave's planes and keypoints equal those
+    of the full build from the same fp64 base, bit for bit; the seed-only
+    octaves have no planes.  960x540 O6 S5: octave-4/5 radii 94 / 188 exceed
+    their planes (clamped chains)."""
+    import torch
+    W, H, O, S = 960, 540, 6, 5
+    img = blob_image(W, H, seed=23)
+    gpu_ctx.detect(img, sift_amd.make_params(1, S, flags=sift_amd.F_EXPORT_NEXT_SEED))
+    d_seed = torch.tensor(gpu_ctx.next_seed(), dtype=torch.float64, device="cuda:0").contiguous()
+    torch.cuda.synchronize()
+    p = sift_amd.make_params(t + 1, S, flags=sift_amd.F_KEYPOINT_ORIGINS)
+    gpu_ctx.detect_from_seed_device(d_seed.data_ptr(), 1, W, H, p)
+    full = gpu_ctx.keypoints().copy()
+    full_org = gpu_ctx.keypoint_origins()
+    planes = [gpu_ctx.plane(k, t, s) for k, n in ((sift_amd.PLANE_GAUSS, S + 3), (sift_amd.PLANE_DOG, S + 2))
+              for s in range(n)]
+    gpu_ctx.detect_from_seed_range_device(d_seed.data_ptr(), 1, t, W, H, p)
+    got = gpu_ctx.keypoints().copy()
+    assert got.tobytes() == full[full_org[:, 0] == t].tobytes()
+    again = [gpu_ctx.plane(k, t, s) for k, n in ((sift_amd.PLANE_GAUSS, S + 3), (sift_amd.PLANE_DOG, S + 2))
+             for s in range(n)]
+    for a, b in zip(planes, again):
+        assert a.tobytes() == b.tobytes()
+    with pytest.raises(sift_amd.SiftError):
+        gpu_ctx.plane(sift_amd.PLANE_DOG, t - 1, 0)
+
+
 def test_loaded_dog_after_range_detection_scans_every_octave(gpu_ctx):
     """A context that ran sift_detect_from_seed_range_device (which scans only
     octaves >= its octave_scan_first) and then loads a caller DoG pyramid

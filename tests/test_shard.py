@@ -221,14 +221,15 @@ class FakeDeviceCtx(FakeCtx):
     def merge_keypoint_blocks_device(self, d_in, counts, d_out):
         import ctypes
         counts = np.asarray(counts, dtype=np.int64)
-        n = int(counts.sum())
+        n = int(np.abs(counts).sum())
         buf = np.frombuffer(ctypes.string_at(d_in, n * 48), dtype=np.uint8).reshape(n, 48)
         parts, off = [], 0
         for q in range(counts.shape[0]):
             blocks = []
             for b in range(counts.shape[1]):
-                blocks.append(buf[off:off + counts[q, b]])
-                off += counts[q, b]
+                c = counts[q, b]
+                blocks.append(buf[off:off + max(c, 0)])  # negative: skipped padding
+                off += abs(c)
             parts.append(blocks)
         out = np.concatenate([parts[q][b] for b in range(counts.shape[1]) for q in range(counts.shape[0])])
         ctypes.memmove(d_out, out.tobytes(), out.nbytes)

@@ -76,7 +76,9 @@ def t_gather(nbytes_per_rank, world):
         if i >= 2:
             ts.append(time.perf_counter() - t0)
     local = float(np.median(ts)) * 1e3
-    model = nbytes_per_rank * (world - 1) / (xgmi * 1e9) * 1e3  # bytes received from the other ranks
+    # the world-1 call's own time (launch + copy: the latency floor) + the
+    # bytes received from the other ranks at the modelled xGMI rate
+    model = local + nbytes_per_rank * (world - 1) / (xgmi * 1e9) * 1e3
     return local, model
 
 
@@ -120,7 +122,8 @@ print(json.dumps({"config": "8K 7680x4320 O6 S5, device-resident (image in HBM, 
                   "critical_path_serial_gathers_ms": round(crit_serial, 3),
                   "critical_path_note": "every tail octave starts from the gathered base: slowest band + base "
                                         "all-gather (model) + max(slowest tail octave + tail-keypoint all-gather, "
-                                        "band-keypoint all-gather running beside the tail) (models) + concatenation "
-                                        "and block merge",
+                                        "band-keypoint all-gather running beside the tail) (models: world-1 call time + bytes "
+                                        "from the other ranks at xgmi_GBps_model) + the two block merges of the padded "
+                                        "gathered lists",
                   "speedup_vs_whole": round(1e3 * float(np.median(t_whole)) / crit, 2),
                   "keypoints": n_whole, "identical": bool(same)}))
