@@ -63,7 +63,10 @@ constexpr int kXW = 62;      // output columns per extrema wave (lanes 1..62; la
 #define SIFT_XROWS 30
 #endif
 constexpr int kXRows = SIFT_XROWS;  // centre rows per extrema wave (multiple of 3)
-constexpr int kXMaxGroup = 5;// scales per extrema wave (S > 5 splits the scales into groups)
+#ifndef SIFT_XMAXGROUP
+#define SIFT_XMAXGROUP 5
+#endif
+constexpr int kXMaxGroup = SIFT_XMAXGROUP;// scales per extrema wave (S > 5 splits the scales into groups)
 
 // One launch scans every octave: unit u (one wave) = (octave, strip of kXRows
 // rows, 62-column word, scale group).
