@@ -1099,6 +1099,7 @@ static int refine_enqueue(sift_ctx* ctx) {
     HIPCHK(launch_refine_fast(P, R, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev_heavy, ctx->stream));  // the rest is latency-bound tail work
     // Uncertain decisions exist only with fp32-rounded native planes.
+    R.wide_exact = ctx->o_first > 0;  // a tail piece (sift_detect_from_seed*): latency over throughput
     if (ctx->dog_source == kNative) HIPCHK(launch_refine_exact(P, R, ctx->stream));
     HIPCHK(launch_status_to_keep(P, R.status, R.cand_key, ctx->keep.as<unsigned>(), R.n, cap, ctx->own_lo,
                                  ctx->own_hi, cnt + kBlk, ctx->stream));

@@ -162,6 +162,7 @@ struct RefineLaunch {
   unsigned* uncertain;// indices for the exact pass
   unsigned* counters; // [3] n uncertain, [4] n singular
   const unsigned* perm; // processing order: thread t refines slot perm[t] (nullptr = slot t)
+  int wide_exact;       // k_refine_exact: 256 threads per patch (latency) instead of one wave (throughput)
 };
 
 // Processing order of the fast refinement (band_order): the slots of the

@@ -353,15 +353,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   }
 }
 
-// One block of kExactRefineThreads per uncertain candidate (persistent over
-// the device-side count): exact fp64 patches (dog_patch, the block's threads
-// share each patch's vertical chains), thread 0 decides.  Polish entries (kPolish: every
+// One block of NT threads per uncertain candidate (persistent over the
+// device-side count): exact fp64 patches (dog_patch, the block's threads
+// share each patch's vertical chains), thread 0 decides.  NT = 64 (one wave)
+// for whole-image detections, whose exact pass runs beside other images'
+// kernels (4K pipelined: 7.18-7.27 vs 7.06-7.16 Gpix/s with 256); NT = 256
+// where it is alone on the critical path (the tail pieces of a sharded image,
+// RefineLaunch::wide_exact): at radius 47 one wave's lanes walk ~15 chains of
+// 95 dependent loads in turn (4K isolated 117 vs 60 us).  Polish entries (kPolish: every
 // decision of the fast pass was certain, only the kept keypoint's output was
 // not precise enough) recompute just the candidate's exact value (omega uses
 // it, background.js:565) and the final position's patch.
-constexpr int kExactRefineThreads = 256;
-
-__global__ __launch_bounds__(kExactRefineThreads) void k_refine_exact(const Pyramid P, const RefineLaunch L) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_refine_exact(const Pyramid P, const RefineLaunch L) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int pos[4];
   const unsigned nu = min(L.counters[3], (unsigned)L.cap);
@@ -377,11 +381,11 @@ __global__ __launch_bounds__(kExactRefineThreads) void k_refine_exact(const Pyra
     double value = 0;
     int status = kRefDiscard;
     if (e & kPolish) {
-      dog_patch<kExactRefineThreads>(P, im, o, s, m, n, sh, Lbuf, d27);
+      dog_patch<NT>(P, im, o, s, m, n, sh, Lbuf, d27);
       value = d27[13];  // all lanes: d27 is visible after the patch's barrier
       const Keypoint& k = L.kp[i];
       const int s1 = k.scale_level, m1 = k.local_y, n1 = k.local_x;
-      if (s1 != s || m1 != m || n1 != n) dog_patch<kExactRefineThreads>(P, im, o, s1, m1, n1, sh, Lbuf, d27);
+      if (s1 != s || m1 != m || n1 != n) dog_patch<NT>(P, im, o, s1, m1, n1, sh, Lbuf, d27);
       if (threadIdx.x == 0) {
         const StepOut R = refine_step<false>(d27, o, s1, m1, n1, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr,
                                              false, 0.0);
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(kExactRefineThreads) void k_refine_exact(const Pyra
       // not kept on exact values (cannot happen with certain decisions): the whole chain
     }
     for (int it = 0; it < 5; ++it) {
-      dog_patch<kExactRefineThreads>(P, im, o, s, m, n, sh, Lbuf, d27);
+      dog_patch<NT>(P, im, o, s, m, n, sh, Lbuf, d27);
       if (threadIdx.x == 0) {
         if (it == 0) value = d27[13];  // exact fp64 candidate value (:565 uses it)
         const StepOut R = refine_step<false>(d27, o, s, m, n, value, 0.0, 0.0, P.S, P.ND, oc.h, oc.w, P.thr, it == 4,
@@ -705,11 +709,13 @@ hipError_t launch_refine_exact(const Pyramid& P, const RefineLaunch& R, hipStrea
   if (R.cap <= 0) return hipSuccess;
   const int grid = std::max(1, std::min(R.cap, 8192));
   const size_t lds = exact_lds_bytes(P);
+  const void* fn = R.wide_exact ? (const void*)k_refine_exact<256> : (const void*)k_refine_exact<64>;
   if (lds > 64 * 1024) {  // scratch of radii above ~335
-    const hipError_t e = hipFuncSetAttribute((const void*)k_refine_exact, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_refine_exact, dim3(grid), dim3(kExactRefineThreads), lds, st, P, R);
+  if (R.wide_exact) hipLaunchKernelGGL(k_refine_exact<256>, dim3(grid), dim3(256), lds, st, P, R);
+  else hipLaunchKernelGGL(k_refine_exact<64>, dim3(grid), dim3(64), lds, st, P, R);
   return hipGetLastError();
 }
 
