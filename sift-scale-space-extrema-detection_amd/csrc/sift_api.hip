@@ -766,7 +766,8 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
   // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
   const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
-  HIPCHK(hipMemsetAsync(cnt, 0, 32 * sizeof(unsigned), st));  // extrema and refinement counters
+  // extrema and refinement counters and the refinement's per-block counts: one fill
+  HIPCHK(hipMemsetAsync(cnt, 0, kCntAll * sizeof(unsigned), st));
   ctx->counters_zeroed = true;
   HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), st));
   ExtremaLaunch& L = ctx->xl;
@@ -994,8 +995,8 @@ static int refine_enqueue(sift_ctx* ctx) {
     HIPCHK(hipMemsetAsync(cnt + kCntUnc, 0, 2 * sizeof(unsigned), ctx->stream));
     HIPCHK(hipMemsetAsync(cnt + kCntKp, 0, sizeof(unsigned), ctx->stream));
     HIPCHK(hipMemsetAsync(cnt + 16, 0, 16 * sizeof(unsigned), ctx->stream));
+    HIPCHK(hipMemsetAsync(cnt + kBlk, 0, (kCntAll - kBlk) * sizeof(unsigned), ctx->stream));
   }
-  HIPCHK(hipMemsetAsync(cnt + kBlk, 0, (kCntAll - kBlk) * sizeof(unsigned), ctx->stream));
   ctx->counters_zeroed = false;
   ctx->n_kp = 0;
   ctx->n_sing = 0;
