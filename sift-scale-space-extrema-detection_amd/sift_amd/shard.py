@@ -509,6 +509,28 @@ def gather_rows(t, counts, group=None):
     return gather_rows_finish(gather_rows_start(t, counts, group))
 
 
+_SIDE_GROUPS = {}
+
+
+def side_group(group=None):
+    """A second communicator over the ranks of `group` (created collectively
+    on first use; every rank calls detect_sharded_device).  RCCL runs the
+    collectives of one communicator in issue order on one stream, so the band
+    keypoints' all-gather (10.9 MB per rank at 8K) issued on the main group
+    would hold back the base all-gather every tail octave waits for; on its
+    own communicator it runs beside the base gather and the tail octaves."""
+    import torch.distributed as dist
+    key = id(group) if group is not None else None
+    g = _SIDE_GROUPS.get(key)
+    if g is None:
+        if group is None:
+            g = dist.new_group()
+        else:  # only the group's ranks call this
+            g = dist.new_group(ranks=dist.get_process_group_ranks(group), use_local_synchronization=True)
+        _SIDE_GROUPS[key] = g
+    return g
+
+
 def _gather_counts(cnt, world, group, dev):
     """Every rank's per-(octave, scale) block counts (int64 [world, O*S] host)."""
     import torch
@@ -543,12 +565,14 @@ def detect_sharded_device(ctx, d_img, params, group=None, max_overhead=0.5, time
         kp, cnt, seed = torch.zeros((0, REC), dtype=torch.uint8, device=dev), np.zeros(0, np.int64), None
     t0 = _tick(timer, "band", t0)
     # The band keypoints' all-gather starts as soon as the bands are done and
-    # runs on RCCL's stream while the tail octaves run on the library's; only
-    # the (few) tail keypoints are gathered after the tail.  The merge takes
-    # the band parts, then the tail parts: no block holds both (the tail
-    # octaves are K+1..O-1), so block-major-then-part order is unchanged.
+    # runs on its own communicator (side_group: its own RCCL stream) while the
+    # base all-gather and the tail octaves run; only the (few) tail keypoints
+    # are gathered after the tail.  The merge takes the band parts, then the
+    # tail parts: no block holds both (the tail octaves are K+1..O-1), so
+    # block-major-then-part order is unchanged.
     band_counts = _gather_counts(_blocks(cnt, O, S), world, group, dev)
-    band = gather_rows_start(kp, [int(c) for c in band_counts.sum(axis=1)], group)
+    band = gather_rows_start(kp, [int(c) for c in band_counts.sum(axis=1)],
+                             side_group(group) if plan.has_tail else group)
     nb_kp = int(band_counts.sum())
     if not plan.has_tail:
         band[0].wait()

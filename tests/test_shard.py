@@ -264,11 +264,25 @@ def _worker_device(rank, world, port, shape, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("shape", [(480, 360, 4, 3), (7680, 4320, 6, 5)])
-def test_detect_sharded_device_gathers_world2(shape):
+@pytest.mark.parametrize("shape,world", [((480, 360, 4, 3), 2), ((7680, 4320, 6, 5), 2),
+                                         ((7680, 4320, 6, 5), 3), ((1920, 1080, 5, 5), 3),
+                                         ((7680, 4320, 6, 5), 8), ((480, 360, 4, 3), 8)])
+def test_detect_sharded_device_gathers(shape, world):
     """The device-resident driver's gathers (all_gather_into_tensor of the
-    padded base rows, counts, records and origins) over gloo, world size 2."""
-    world = 2
+    padded base rows, counts, records and origins; the band keypoints on a
+    second communicator) over gloo at world sizes 2, 3 and 8.  At 8K O6 on 8
+    ranks three ranks own the tail octaves 3/4/5 and five own bands only, and
+    the merge interleaves 8 parts block-major: patterns world size 2 cannot
+    exercise."""
+    from sift_amd.shard import plan_bands, tail_octaves
+    W, H, O, S = shape
+    plan = plan_bands(W, H, sift_amd.make_params(O, S), world, 0.5)
+    owners = set(tail_octaves(plan, world).values()) if plan.has_tail else set()
+    assert len(plan.bands) == world
+    if world >= 3:
+        assert len(owners) >= 2  # several tail owners
+    if world == 8:
+        assert len(owners) < world  # and band-only ranks
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
