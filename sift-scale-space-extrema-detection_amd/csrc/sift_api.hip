@@ -415,7 +415,9 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
   const bool keep_gauss = !(p->flags & SIFT_F_SKIP_GAUSS_PLANES);
   if (nimg > 1) {
     if (o_first != 0 || (!img_host && !img_dev) || fuse_extrema || gauss_needs_base0(P) || ctx->row0 != 0 ||
-        ctx->own_lo >= 0 || (p->flags & (SIFT_F_EXPORT_NEXT_SEED | SIFT_F_LOW_CONTRAST_LIST | SIFT_F_FUSED_EXTREMA)))
+        ctx->own_lo >= 0 ||
+        (p->flags & (SIFT_F_EXPORT_NEXT_SEED | SIFT_F_LOW_CONTRAST_LIST | SIFT_F_FUSED_EXTREMA |
+                     SIFT_F_KEYPOINT_ORIGINS)))  // origins carry no image index
       return set_err(ctx, SIFT_E_UNSUPPORTED, "batch: whole device images, plain detection only");
     if ((unsigned long long)P.kpi * (unsigned long long)nimg > 0xffffffffull ||
         (long long)nimg * P.O * P.S > kBlkN)

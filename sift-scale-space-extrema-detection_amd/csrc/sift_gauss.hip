@@ -115,7 +115,7 @@ struct GTile {
   int bx;              // tile column
   int lane, wv;        // wv wave-uniform (SGPR)
   int cg, rs;          // horizontal mapping (64-column tiles)
-  int icg[3], irow[3]; // 96-column tiles: item i of the lane = columns 4 icg .. +3 of wave row irow
+  int icg[4], irow[4]; // 96- / 128-column tiles: item i of the lane = columns 4 icg .. +3 of wave row irow
   int sw;              // strip stride
   int hrm;             // octave 0: ceil(RM / 2) of the staged region
   const double* S0;    // octave 0: staged input region [..][kBW0]
@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
   T.rs = T.lane / kCG;
   if constexpr (TW == 96) {
 #if SIFT_B128MAP
-    int g, j;  // conflict-free ds_read_b128 item map (k_gauss_lds)
+    int g, j;  // conflict-free ds_read_b128 item map
     b128_group(T.lane, g, j);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -1241,479 +1241,376 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
 }
 
 // ---------------------------------------------------------------------------
-// Producer / consumer waves (octaves >= 1).  In k_gauss_dog every wave runs
-// its scale loop as vertical pass (base loads: TA / L2 bound) -> horizontal
-// pass -> plane stores (LDS / HBM-store bound), and the waves of a CU move
-// through these phases together, so the phases add up instead of
-// overlapping; each scale's first base load also waits behind the previous
-// scale's stores (vmcnt counts both, in issue order).  Here a block has 8
-// waves for a TW x 32 tile: waves 0-3 (producers) run the vertical passes
-// of rows 8 w .. 8 w + 7 into one of two strips, waves 4-7 (consumers) run
-// the horizontal passes and the epilogue of the same rows from the other
-// strip, one scale behind:
-//
-//   producers  V(s0) | V(s0+1) | V(s0+2) | ...
-//   consumers        | H(s0)   | H(s0+1) | ...     (one LDS barrier per scale)
-//
-// so every CU always has load-bound and store-bound work in flight, and the
-// producers never store (their loads wait for nothing else) nor the
-// consumers load from global memory.  Same strips, same fma chains per
-// output as k_gauss_dog (bit-identical planes).
+// Register-window tiles for octaves >= 1 (k_gauss_rw).  k_gauss_dog re-reads
+// its fp64 base window from L1/L2 once per SCALE (S+3 times) and every wave
+// re-reads the 2r rows it shares with the waves above and below: at 4K the
+// active blocks of an XCD need ~4 MiB of base lines, its L2 holds 40-60 % of
+// those re-reads and the rest stream from the Infinity Cache at ~7 TB/s,
+// which bounds the vertical pass (the same loop from an L2-resident plane or
+// from LDS issues fp64 fmas 3-4x faster: profiles/r4_fma_probe.txt).  Here
+// every lane of a 256-lane block owns ONE strip column and keeps that
+// column's window of 8 + 2 RW base rows in registers for ALL scales of the
+// octave (RW >= the octave's largest radius): each base value is loaded once
+// per block, and the vertical pass of every scale is register fmas only,
+//   V[t][c] = sum_k w_k win_c[t + k + RW - r],  t < 8,
+// taps in increasing order from 0.0 (k_gauss_dog's chain).  Strip column c
+// <-> image column x0 - RW + c, so the 256 columns hold the vertical sums of
+// an output tile of TW = 224 (RW <= 16) or 192 (RW <= 32) columns and its
+// halo for every radius <= RW: no separate halo pass.  The strip (8 rows,
+// double-buffered in LDS) is shared by the block's 4 waves: one barrier per
+// scale.  Horizontal pass: items of 8 columns x 1 row (8 fma chains per
+// lane); the items of a ds_read_b128 lane group are 4 column groups x 4 rows
+// (strip stride 2 mod 4 doubles: conflict-free).  Same fma chain per output
+// as k_gauss_dog: bit-identical planes.
 // ---------------------------------------------------------------------------
-template <int TW, int RMAX>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_gauss_ws(const Pyramid P,
-                                                                                      const GaussLaunch L) {
-  constexpr int NI = TW == kGX ? kNR : 3;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const Octave& oc = P.oct[L.o];
-  int lb = blockIdx.x;
-  if (L.xcd_band) {
-    const int nb = L.gx * L.gy * L.G, q = nb >> 3, rm = nb & 7, xc = lb & 7;
-    lb = xc * q + min(xc, rm) + (lb >> 3);
-  }
-  const int bz = lb % L.G, bt = lb / L.G;
-  const int bx = bt % L.gx, by = bt / L.gx;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool producer = wave < 4;
-  GTile T;
-  T.bx = bx;
-  T.h = oc.h;
-  T.w = oc.w;
-  T.x0 = bx * TW;
-  T.y0 = by * kGY;
-  T.lane = threadIdx.x & 63;
-  T.wv = wave & 3;  // slab: rows 8 wv .. 8 wv + 7 of the tile
-  T.cg = T.lane & (kCG - 1);
-  T.rs = T.lane / kCG;
-  if constexpr (TW == 96) {
-    int g, j;  // conflict-free ds_read_b128 item map
-    b128_group(T.lane, g, j);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      T.icg[i] = 8 * i + (j & 7);
-      T.irow[i] = 2 * g + (j >> 3);
-    }
-  }
-  auto irw = [&](int i) { return TW == kGX ? T.rs + kRS * i : T.irow[i]; };
-  auto icg = [&](int i) { return TW == kGX ? T.cg : T.icg[i]; };
-  T.sw = L.sw;
-  T.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L.base), 0, T.h * T.w * 8, 0x00020000);
-  const int nstrip = kGY * T.sw;
-  if (L.zero)
-    for (int i = threadIdx.x; i < 2 * nstrip; i += 512) smem[i] = 0.0;
-  const long long plane = (long long)T.h * T.w;
-  const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
-  const int s_first = max(0, s_begin - 1);
-  __syncthreads();  // zeroed strips
+template <int RW>
+struct RwGeom {
+  static constexpr int NW = 8 + 2 * RW;              // window rows per lane
+  static constexpr int TW = RW <= 16 ? 224 : 192;     // output columns per tile
+  static constexpr int NCG = TW / 4;                  // column groups of 4
+  static_assert(2 * RW <= 256 - TW, "halo fits the strip");
+};
+constexpr int kRwRows = 8;    // output rows per tile
+constexpr int kRwSW = 264;    // strip row stride (doubles), 0 mod 8
+constexpr int kRwStrip = kRwRows * kRwSW + 8;  // doubles per strip buffer
+// Strip row t starts at rw_row(t): rows 4..7 one 16-byte quad further, so a
+// ds_read_b128 lane group reading 8 column groups of rows t and t + 4 hits
+// 16 distinct bank quads.
+__host__ __device__ constexpr int rw_row(int t) { return t * kRwSW + 2 * (t >> 2); }
+#ifndef SIFT_RWPF
+#define SIFT_RWPF 3  // 16-byte strip reads in flight per row, horizontal pass
+#endif
+#ifndef SIFT_RWTAPS
+#define SIFT_RWTAPS 8  // taps per reload of the tap pointer (0: never: the compiler keeps them in SGPRs)
+#endif
+#ifndef SIFT_RW_WPE
+#define SIFT_RW_WPE 1  // minimum waves per SIMD the register allocation must allow
+#endif
 
-  const bool st = !(L.dbg & 1);
-  int voff[NI];
-  bool own[NI];
+// Vertical pass of one strip column: acc[t] = sum_k w_k win[t + k + RW - R].
+// Tap loads: the tap pointer is made opaque every 8 taps, so the compiler
+// loads each group of taps where it is used instead of keeping 2r + 1 taps
+// in SGPRs.
+template <int R, int RW>
+__device__ __forceinline__ void rw_vert(const double (&win)[RwGeom<RW>::NW], const cdouble* wp, double (&acc)[8]) {
+  constexpr int D = RW - R;
+  const cdouble* wq = wp;
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int y = T.y0 + 8 * T.wv + irw(i);
-    const int x = T.x0 + 4 * icg(i);
-    own[i] = y < T.h && T.w - x > 0;
-    voff[i] = own[i] ? (y * T.w + x) * 4 : 0x7ffffff0;
-  }
-  // Separate loops (the same number of barriers on both sides): no value of
-  // one role is live in the other's code.
-  if (producer) {  // scale s into strip s & 1, one scale ahead of the consumers
-    for (int s = s_first; s < s_end; ++s) {
-      double* V = smem + (s & 1) * nstrip;
-      GTile Ts = T;
-      asm volatile("" : "+v"(Ts.lane));
-      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
-      if (L.vsplit) vert_copy(Ts, oc.rad[s], L.vsplit + (long long)s * plane, V);
-      else if constexpr (TW == 96) vert96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V);
-      else vert_any<false, RMAX>(Ts, oc.rad[s], wp, V);
-      lds_barrier();  // strip s written; strip s - 1 read by the consumers
-    }
-    lds_barrier();
-    return;
-  }
-  lds_barrier();  // the producers' first strip
-  double lprev[NI][4];
-  const int nS = P.S;
-  for (int s = s_first; s < s_end; ++s) {
-    if constexpr (TW == 96) {
-      // items 0-1 side by side, then 2, each group with its epilogue (only
-      // one group's chains and reads live: k_gauss_dog's SIFT_TW96_SEQ 2)
-      const double* V = smem + (s & 1) * nstrip;
-      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
-      GTile Ts = T;
-      asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
-      const unsigned pb = (unsigned)plane * 4u;
-      const bool stor = s >= s_begin && st;
-      const __amdgpu_buffer_rsrc_t rg =
-          __builtin_amdgcn_make_buffer_rsrc(L.gauss ? L.gauss + s * plane : L.dog, 0, pb, 0x00020000);
-      const __amdgpu_buffer_rsrc_t rd =
-          __builtin_amdgcn_make_buffer_rsrc(L.dog + (s > 0 ? s - 1 : 0) * plane, 0, pb, 0x00020000);
-      horz96s_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V,
-                   [&](int i, const double (&o)[4]) {
-                     double d[4];
+  for (int t = 0; t < 8; ++t) acc[t] = 0.0;
 #pragma unroll
-                     for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[q];
-                     const int y = T.y0 + 8 * T.wv + irw(i);
-                     const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
-                     if (stor) {
-                       if (L.vec) {
-                         if (L.gauss) bstore4(rg, voff[i], o);
-                         if (s > 0) bstore4(rd, voff[i], d);
-                       } else if (own[i]) {
-                         const long long pp = (long long)y * T.w + x;
-                         if (L.gauss) store4(L.gauss + s * plane + pp, o, nvalid);
-                         if (s > 0) store4(L.dog + (s - 1) * plane + pp, d, nvalid);
-                       }
-                     }
-                     if (s == nS && L.next_seed && s >= s_begin && own[i] && !(y & 1)) {
-                       double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
-                       sd[0] = o[0];
-                       if (nvalid > 2) sd[1] = o[2];
-                     }
+  for (int k = 0; k <= 2 * R; ++k) {
+    if (SIFT_RWTAPS > 0 && k % (SIFT_RWTAPS > 0 ? SIFT_RWTAPS : 1) == 0) asm volatile("" : "+s"(wq));
+    const double wk = wq[k];
 #pragma unroll
-                     for (int q = 0; q < 4; ++q) lprev[i][q] = o[q];
-                   });
-    } else {
-      const double* V = smem + (s & 1) * nstrip;
-      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
-      GTile Ts = T;
-      asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
-      double out[NI][4];
-      if constexpr (TW == 96) horz96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V, out);
-      else horz_any<false, RMAX>(Ts, oc.rad[s], wp, V, out);
-      double d[NI][4];
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
-      if (s >= s_begin && (st || out[0][0] == 12345.0)) {
-        if (L.vec) {
-          const unsigned pb = (unsigned)plane * 4u;
-          if (L.gauss) {
-            const __amdgpu_buffer_rsrc_t rg =
-                __builtin_amdgcn_make_buffer_rsrc(L.gauss + s * plane, 0, pb, 0x00020000);
-#pragma unroll
-            for (int i = 0; i < NI; ++i) bstore4(rg, voff[i], out[i]);
-          }
-          if (s > 0) {
-            const __amdgpu_buffer_rsrc_t rd =
-                __builtin_amdgcn_make_buffer_rsrc(L.dog + (s - 1) * plane, 0, pb, 0x00020000);
-#pragma unroll
-            for (int i = 0; i < NI; ++i) bstore4(rd, voff[i], d[i]);
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < NI; ++i) {
-            const int y = T.y0 + 8 * T.wv + irw(i);
-            const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
-            if (own[i]) {
-              const long long pp = (long long)y * T.w + x;
-              if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
-              if (s > 0) store4(L.dog + (s - 1) * plane + pp, d[i], nvalid);
-            }
-          }
-        }
-      }
-      if (L.l64 && s >= s_begin) {  // fp64 plane for the exact passes
-        double* lp = L.l64 + s * plane;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int y = T.y0 + 8 * T.wv + irw(i);
-          const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
-          if (own[i]) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (q < nvalid) lp[(long long)y * T.w + x + q] = out[i][q];
-          }
-        }
-      }
-      if (s == P.S && L.next_seed && s >= s_begin) {
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int y = T.y0 + 8 * T.wv + irw(i);
-          const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
-          if (own[i] && !(y & 1)) {
-            double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
-            sd[0] = out[i][0];
-            if (nvalid > 2) sd[1] = out[i][2];
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
-    }
-    lds_barrier();  // strip s read by the consumers, strip s + 1 written by the producers
+    for (int t = 0; t < 8; ++t) acc[t] = fma(wk, win[t + k + D], acc[t]);
   }
 }
 
-// ---------------------------------------------------------------------------
-// LDS-resident base (octaves >= 1 whose base region and strip fit one CU's
-// LDS: 4K / 8K octaves 1 and 2).  k_gauss_dog's octaves >= 1 re-read the
-// base region from L1/L2 once per SCALE: S+3 passes of 16-byte loads whose
-// address processing bounds the launch (TA busy 0.6-0.8), and every scale's
-// first load waits behind the previous scale's plane stores (vmcnt counts
-// loads and stores in issue order).  Here a block owns a TW x 64 tile with 8
-// waves (8 rows each), stages the fp64 base region (64 + 2R rows x TW + 2R
-// columns, edges replicated) in LDS ONCE, and every scale's vertical pass
-// reads it from LDS: no global load after the staging, stores fire and
-// forget.  The price is occupancy (one block = 2 waves per SIMD), paid back
-// with registers: up to 256 VGPRs per lane, so deeper prefetch and more
-// independent fma chains per wave.  Same fma chains per output as the tile
-// kernel (bit-identical planes).
-// ---------------------------------------------------------------------------
-constexpr int kLY = 64;   // tile rows (8 waves x 8)
-constexpr int kLPF = 8;   // LDS rows in flight, vertical pass
-
-// Strip columns c = lane and lane + 64 of the wave's 8 rows for radius R,
-// from the staged region B (row stride BW, region row 0 = tile row -Rm,
-// region column 0 = tile column -Rm): V[t][c] = sum_k w_k B[8 wv + t + k +
-// d][c + d], d = Rm - R.  One double per lane and row: 64 consecutive
-// doubles per ds_read_b64, conflict-free (a 16-byte pair per lane is 8-byte
-// aligned when d is odd: ds_read2_b64 with 2-way conflicts); every row of the
-// window at an immediate offset from one address.
-template <int R, int TW, int BW>
-__device__ __forceinline__ void vert_lds(const GTile& T, int d, const double* B, const cdouble* wp, double* V) {
-  constexpr int NC = TW + 2 * R;
-  constexpr bool TWO = NC > 64;
-  static_assert(NC <= 128, "two columns per lane");
-  constexpr int NJ = 2 * R + 8;
-  constexpr int PF = NJ < kLPF ? NJ : kLPF;
-  if (!TWO && T.lane >= NC) return;
-  const double* src = B + (8 * T.wv + d) * BW + d + T.lane;
-  double a0[8], a1[8];
-  double2 v[NJ];
-  auto ld = [&](int j) -> double2 { return make_double2(src[j * BW], TWO ? src[j * BW + 64] : 0.0); };
+// Horizontal pass of one item (4 columns x rows A, B): out[i][q] = sum_k w_k
+// V[row_i][b + q + k], b = 4 cg + RW - R (strip column of the first tap of
+// output column x0 + 4 cg); 16-byte reads from the even column at or before b.
+template <int R, int RW>
+__device__ __forceinline__ void rw_horz(const double* ra, const double* rb, const cdouble* wp, double (&out)[2][4]) {
+  constexpr int D = (RW - R) & 1;           // b odd: element n is pair (n + 1) / 2, half (n + 1) & 1
+  constexpr int NE = 4 + 2 * R;             // elements n = 0 .. 3 + 2R
+  constexpr int NP = (NE - 1 + D) / 2 + 1;  // pairs per row
+  constexpr int PF = NP < SIFT_RWPF ? NP : SIFT_RWPF;
+  const double* pa = ra + ((RW - R) - D);   // even column
+  const double* pb = rb + ((RW - R) - D);
+  double2 u[2][NP];
+  const cdouble* wq = wp;
 #pragma unroll
-  for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
+  for (int q = 0; q < 4; ++q) out[0][q] = out[1][q] = 0.0;
 #pragma unroll
-  for (int j = 0; j < PF; ++j) v[j] = ld(j);
+  for (int n2 = 0; n2 < PF; ++n2) {
+    u[0][n2] = *reinterpret_cast<const double2*>(pa + 2 * n2);
+    u[1][n2] = *reinterpret_cast<const double2*>(pb + 2 * n2);
+  }
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    if (j + PF < NJ) v[j + PF] = ld(j + PF);
+  for (int n2 = 0; n2 < NP; ++n2) {
+    if (n2 + PF < NP) {
+      u[0][n2 + PF] = *reinterpret_cast<const double2*>(pa + 2 * (n2 + PF));
+      u[1][n2 + PF] = *reinterpret_cast<const double2*>(pb + 2 * (n2 + PF));
+    }
+    if (SIFT_RWTAPS > 0 && n2 % (SIFT_RWTAPS > 0 ? SIFT_RWTAPS / 2 : 1) == 0) asm volatile("" : "+s"(wq));
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int k = j - t;
-      if (k >= 0 && k <= 2 * R) {
-        a0[t] = fma((double)wp[k], v[j].x, a0[t]);
-        if (TWO) a1[t] = fma((double)wp[k], v[j].y, a1[t]);
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * n2 + e - D;  // element index
+      if (n < 0 || n >= NE) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = n - q;
+        if (k >= 0 && k <= 2 * R) {
+          const double wk = wq[k];
+          out[0][q] = fma(wk, e ? u[0][n2].y : u[0][n2].x, out[0][q]);
+          out[1][q] = fma(wk, e ? u[1][n2].y : u[1][n2].x, out[1][q]);
+        }
       }
     }
-    pin(a0);
-    if (TWO) pin(a1);
+    pin(out[0]);
+    pin(out[1]);
   }
-  double* Vw = V + 8 * T.wv * T.sw + T.lane;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) Vw[t * T.sw] = a0[t];
-  if (TWO && T.lane + 64 < NC)
-#pragma unroll
-    for (int t = 0; t < 8; ++t) Vw[t * T.sw + 64] = a1[t];
 }
 
-// Generic radii (up to 32): the 8-row chunks over zero-padded taps of
-// vert_glob_gen (same fma chains), rows from the staged region.
-template <int TW, int BW>
-__device__ __forceinline__ void vert_lds_gen(const GTile& T, int r, int d, const double* B, const cdouble* wp,
-                                             double* V) {
-  const int NC = TW + 2 * r, NJ = 2 * r + 8;
-  const double* src = B + (8 * T.wv + d) * BW + d + T.lane;
-  const bool two = T.lane + 64 < NC;
-  double a0[8], a1[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) a0[t] = a1[t] = 0.0;
-  auto chunk = [&](int jb, auto C, auto first) {
-    using CC = decltype(C);
-    double2 v[8];
-#pragma unroll
-    for (int k = 0; k < CC::kRows; ++k) v[k] = make_double2(src[(jb + k) * BW], src[(jb + k) * BW + 64]);
-    const cdouble* w = wp + jb;
-    CC::template run<decltype(first)::value>([&](int k, int t) {
-      a0[t] = fma((double)w[k - t], v[k].x, a0[t]);
-      a1[t] = fma((double)w[k - t], v[k].y, a1[t]);
-    });
-    pin(a0);
-    pin(a1);
-  };
-  vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
-  for (int jb = 8; jb < NJ; jb += 8)
-    vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
-  double* Vw = V + 8 * T.wv * T.sw + T.lane;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) Vw[t * T.sw] = a0[t];
-  if (two)
-#pragma unroll
-    for (int t = 0; t < 8; ++t) Vw[t * T.sw + 64] = a1[t];
-}
-
-template <int TW, int BW, int... Rs>
-__device__ __forceinline__ void vert_lds_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r, int d,
-                                             const double* B, const cdouble* wp, double* V) {
+template <int RW, int... Rs>
+__device__ __forceinline__ void rw_vert_any_(std::integer_sequence<int, Rs...>, int r,
+                                            const double (&win)[RwGeom<RW>::NW], const cdouble* wp,
+                                            double (&acc)[8]) {
   bool done = false;
-  ((!done && r == Rs ? (vert_lds<Rs, TW, BW>(T, d, B, wp, V), done = true) : false), ...);
-  if (!done) vert_lds_gen<TW, BW>(T, r, d, B, wp, V);
+  ((!done && r == Rs ? (rw_vert<Rs, RW>(win, wp, acc), done = true) : false), ...);
+}
+template <int RW, int... Rs>
+__device__ __forceinline__ void rw_horz_any_(std::integer_sequence<int, Rs...>, int r, const double* ra,
+                                            const double* rb, const cdouble* wp, double (&out)[2][4]) {
+  bool done = false;
+  ((!done && r == Rs ? (rw_horz<Rs, RW>(ra, rb, wp, out), done = true) : false), ...);
 }
 
-// Region row stride (doubles) of the staged base: TW + 2 Rc columns, Rc the
-// largest octave radius the instance takes (12 for 96-column tiles, whose
-// radii are all unrolled; 23 for 64-column tiles: 4K / 8K octave 2 at S = 5),
-// so every row of a window is an immediate offset.
-__host__ __device__ constexpr int lds_region_stride(int tw) { return tw == 96 ? 96 + 2 * 12 : 64 + 2 * 23; }
-
-template <int TW, int RMAX>
-__global__ __launch_bounds__(512) void k_gauss_lds(const Pyramid P, const GaussLaunch L) {
-  constexpr int BW = lds_region_stride(TW);
-  constexpr int NI = TW == kGX ? kNR : 3;
+template <int RW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE))) void k_gauss_rw(const Pyramid P, const GaussLaunch L) {
+  using G = RwGeom<RW>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const Octave& oc = P.oct[L.o];
+  // 1D grid: block -> (scale group, tile) as in k_gauss_dog (XCD bands, batches image-major).
   int lb = blockIdx.x;
+  const int bpi = L.gx * L.gy * L.G;
   if (L.xcd_band) {
-    const int nb = L.gx * L.gy * L.G, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    const int nb = bpi * L.nimg, q = nb >> 3, rm = nb & 7, xc = lb & 7;
     lb = xc * q + min(xc, rm) + (lb >> 3);
   }
+  const int im = lb / bpi;
+  lb -= im * bpi;
+  float* const L_gauss = L.gauss ? L.gauss + im * L.gauss_bs : nullptr;
+  float* const L_dog = L.dog + im * L.dog_bs;
+  double* const L_next_seed = L.next_seed ? L.next_seed + im * L.seed_bs : nullptr;
+  const double* const L_base = L.base + im * L.base_bs;
   const int bz = lb % L.G, bt = lb / L.G;
-  const int bx = bt % L.gx, by = bt / L.gx;
-  GTile T;
-  T.bx = bx;
-  T.h = oc.h;
-  T.w = oc.w;
-  T.x0 = bx * TW;
-  T.y0 = by * kLY;
-  T.lane = threadIdx.x & 63;
-  T.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  T.cg = T.lane & (kCG - 1);
-  T.rs = T.lane / kCG;
-  if constexpr (TW == 96) {
-    // item i of lane (group g, position j): columns 4 (8 i + j % 8) .. + 3
-    // of wave row 2 g + j / 8 -- in every 16-lane group of a ds_read_b128
-    // the 8 column groups of two adjacent rows (strip stride 2 mod 4
-    // doubles): 16 distinct bank quads, conflict-free.
-    int g, j;
-    b128_group(T.lane, g, j);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      T.icg[i] = 8 * i + (j & 7);
-      T.irow[i] = 2 * g + (j >> 3);
-    }
-  }
-  auto irw = [&](int i) { return TW == kGX ? T.rs + kRS * i : T.irow[i]; };
-  auto icg = [&](int i) { return TW == kGX ? T.cg : T.icg[i]; };
-  T.sw = L.sw;
-  const int Rm = oc.rmax;
-  constexpr int bw = BW;
-  double* V = smem;
-  double* B = smem + kLY * T.sw;
-
-  if (L.zero)
-    for (int i = threadIdx.x; i < kLY * T.sw; i += 512) smem[i] = 0.0;
+  const int bx = bt % L.gx, by = bt / L.gx + L.by0;
+  const int h = oc.h, w = oc.w;
+  const int x0 = bx * G::TW, y0 = by * kRwRows;
+  const int c = threadIdx.x;  // strip column
+  // The lane's base window: rows y0 - RW .. y0 + 7 + RW of image column x0 - RW + c (clamped).
+  double win[G::NW];
   {
-    // Stage base rows y0 - Rm .. y0 + 63 + Rm, columns x0 - Rm .. x0 + TW +
-    // Rm - 1, clamped (replicate edges): one 16-byte load per column pair
-    // (pair x, x+1 read at clamp(x, 0, w-2), edge pairs selected as in
-    // vert_glob2), all of a wave's rows in flight before its LDS writes.
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L.base), 0, T.h * T.w * 8, 0x00020000);
-    const int nrr = kLY + 2 * Rm, npair = (TW + 2 * Rm) / 2;
-    const int x = T.x0 - Rm + 2 * T.lane;
-    const int xoff = clampi(x, 0, T.w - 2) * 8;
-    const bool lo_edge = x < 0, hi_edge = x >= T.w - 1;
-    constexpr int kMaxRows = (kLY + 2 * 32 + 7) / 8;  // region rows per wave (radii up to 32)
-    double2 v[kMaxRows];
-    if (T.lane < npair) {
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
+    const int xoff = clampi(x0 - RW + c, 0, w - 1) * 8;
 #pragma unroll
-      for (int i = 0; i < kMaxRows; ++i) {
-        const int rr = T.wv + 8 * i;
-        if (rr < nrr) {
-          const int yy = clampi(T.y0 - Rm + rr, 0, T.h - 1);
-          v[i] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, xoff, yy * T.w * 8, 0));
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < kMaxRows; ++i) {
-        const int rr = T.wv + 8 * i;
-        if (rr < nrr)
-          *reinterpret_cast<double2*>(B + rr * bw + 2 * T.lane) =
-              make_double2(hi_edge ? v[i].y : v[i].x, lo_edge ? v[i].x : v[i].y);
-      }
-    }
+    for (int j = 0; j < G::NW; ++j)
+      win[j] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(y0 - RW + j, 0, h - 1) * w * 8));
   }
-  const long long plane = (long long)T.h * T.w;
-  bool own[NI];
-  int voff[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int y = T.y0 + 8 * T.wv + irw(i);
-    const int x = T.x0 + 4 * icg(i);
-    own[i] = y < T.h && T.w - x > 0;
-    voff[i] = own[i] ? (y * T.w + x) * 4 : 0x7ffffff0;
+  // Horizontal items of 4 columns x 2 rows: ds_read_b128 lane group gid =
+  // 4 wv + g (b128_group) at position j: column group cg = 8 (gid >> 1) +
+  // (j & 7), rows a = gid & 1 or 2 + (gid & 1) and a + 4, the half-groups in
+  // opposite order (j < 8: a = gid & 1 first; j >= 8: a + 4 first), so every
+  // read instruction covers two rows 6 or 2 apart (odd quad offsets through
+  // rw_row: conflict-free) and every store instruction 128 contiguous bytes
+  // of a row per half-group.
+  int hcg, hr0, hr1;
+  {
+    int g, j;
+    b128_group(c & 63, g, j);
+    const int gid = 4 * (c >> 6) + g;
+    hcg = 8 * (gid >> 1) + (j & 7);
+    hr0 = j < 8 ? (gid & 1) : 6 + (gid & 1);
+    hr1 = j < 8 ? 4 + (gid & 1) : 2 + (gid & 1);
   }
+  const bool hact = hcg < G::NCG;  // lanes with an item
+  const long long plane = (long long)h * w;
   const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
   const int s_first = max(0, s_begin - 1);
-  __syncthreads();  // staged region / zeroed strip visible to every wave
-
-  const bool st = !(L.dbg & 1);
-  double lprev[NI][4];
+  const bool st = !(L.dbg & 1);  // dbg 1: timing without plane stores
+  double lprev[2][4];
   for (int s = s_first; s < s_end; ++s) {
     const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
-    GTile Ts = T;
-    asm volatile("" : "+v"(Ts.lane), "+v"(Ts.cg), "+v"(Ts.rs));
     const int r = oc.rad[s];
-    vert_lds_any_<TW, BW>(std::make_integer_sequence<int, RMAX + 1>{}, Ts, r, Rm - r, B, wp, V);
-    wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
-    double out[NI][4];
-    if constexpr (TW == 96) horz96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, r, wp, V, out);
-    else horz_any<false, RMAX>(Ts, r, wp, V, out);
-    wave_lds_fence();  // strip rows read before the next scale overwrites them
-    double d[NI][4];
+    double* Vs = smem + (s & 1) * kRwStrip;
+    {
+      double acc[8];
+      rw_vert_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, r, win, wp, acc);
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
+      for (int t = 0; t < 8; ++t) Vs[rw_row(t) + c] = acc[t];
+    }
+    // Strip s complete; every wave is past its horizontal pass of scale s - 1
+    // (the other buffer), so the next scale may overwrite that one.
+    lds_barrier();
+    if (hact) {
+      int hc = hcg, h0 = hr0, h1 = hr1;
+      asm volatile("" : "+v"(hc), "+v"(h0), "+v"(h1));  // per-scale opaque: no hoisted per-radius addresses
+      double o[2][4];
+      rw_horz_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, r, Vs + rw_row(h0) + 4 * hc,
+                       Vs + rw_row(h1) + 4 * hc, wp, o);
+      const int x = x0 + 4 * hc, nvalid = w - x;
+      const unsigned pb = (unsigned)plane * 4u;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d[i][q] = lprev[i][q] - out[i][q];
-    if (s >= s_begin && (st || out[0][0] == 12345.0)) {
-      if (L.vec) {
-        const unsigned pb = (unsigned)plane * 4u;
-        if (L.gauss) {
-          const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L.gauss + s * plane, 0, pb, 0x00020000);
+      for (int i = 0; i < 2; ++i) {
+        const int y = y0 + (i ? h1 : h0);
+        const bool own = y < h && nvalid > 0;
+        double d[4];
 #pragma unroll
-          for (int i = 0; i < NI; ++i) bstore4(rg, voff[i], out[i]);
-        }
-        if (s > 0) {
-          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L.dog + (s - 1) * plane, 0, pb, 0x00020000);
-#pragma unroll
-          for (int i = 0; i < NI; ++i) bstore4(rd, voff[i], d[i]);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int y = T.y0 + 8 * T.wv + irw(i);
-          const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
-          if (own[i]) {
-            const long long pp = (long long)y * T.w + x;
-            if (L.gauss) store4(L.gauss + s * plane + pp, out[i], nvalid);
-            if (s > 0) store4(L.dog + (s - 1) * plane + pp, d[i], nvalid);
+        for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[i][q];
+        if (s >= s_begin && st) {
+          if (L.vec) {
+            const int voff = own ? (y * w + x) * 4 : 0x7ffffff0;  // dropped past the plane
+            if (L_gauss)
+              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000), voff, o[i]);
+            if (s > 0)
+              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000), voff, d);
+          } else if (own) {
+            const long long pp = (long long)y * w + x;
+            if (L_gauss) store4(L_gauss + s * plane + pp, o[i], nvalid);
+            if (s > 0) store4(L_dog + (s - 1) * plane + pp, d, nvalid);
           }
         }
-      }
-    }
-    if (s == P.S && L.next_seed && s >= s_begin) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int y = T.y0 + 8 * T.wv + irw(i);
-        const int x = T.x0 + 4 * icg(i), nvalid = T.w - x;
-        if (own[i] && !(y & 1)) {
-          double* sd = L.next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
-          sd[0] = out[i][0];
-          if (nvalid > 2) sd[1] = out[i][2];
+        if (s == P.S && L_next_seed && s >= s_begin && own && !(y & 1)) {
+          double* sd = L_next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+          sd[0] = o[i][0];
+          if (nvalid > 2) sd[1] = o[i][2];
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lprev[i][q] = o[i][q];
       }
     }
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) lprev[i][q] = out[i][q];
   }
 }
+
+// Producer / consumer form of k_gauss_rw (k_gauss_pc): a block of 8 waves
+// (2 per SIMD); waves 0-3 hold the register windows and run the vertical
+// passes (register fmas only) into one of two strips, waves 4-7 run the
+// horizontal passes and the stores of the previous scale from the other:
+//   phase p:  V(s0 + p) -> strip p % 2   |   H(s0 + p - 1) <- strip (p - 1) % 2
+// one block barrier per phase.  Each SIMD holds one producer and one
+// consumer wave of the block, so the producer's fmas fill the consumer's
+// LDS and store latency; the two roles run separate loops, so their
+// registers do not add up (the window lives only in the producer's).
+template <int RW>
+__global__ __launch_bounds__(512) void k_gauss_pc(const Pyramid P, const GaussLaunch L) {
+  using G = RwGeom<RW>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Octave& oc = P.oct[L.o];
+  int lb = blockIdx.x;
+  const int bpi = L.gx * L.gy * L.G;
+  if (L.xcd_band) {
+    const int nb = bpi * L.nimg, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    lb = xc * q + min(xc, rm) + (lb >> 3);
+  }
+  const int im = lb / bpi;
+  lb -= im * bpi;
+  const int bz = lb % L.G, bt = lb / L.G;
+  const int bx = bt % L.gx, by = bt / L.gx + L.by0;
+  const int h = oc.h, w = oc.w;
+  const int x0 = bx * G::TW, y0 = by * kRwRows;
+  const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
+  const int s_first = max(0, s_begin - 1);
+  const int nph = s_end - s_first + 1;  // phases
+  if (threadIdx.x < 256) {
+    // producer: strip column c, window rows y0 - RW .. y0 + 7 + RW of image column x0 - RW + c
+    const int c = threadIdx.x;
+    const double* const L_base = L.base + im * L.base_bs;
+    double win[G::NW];
+    {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
+      const int xoff = clampi(x0 - RW + c, 0, w - 1) * 8;
+#pragma unroll
+      for (int j = 0; j < G::NW; ++j)
+        win[j] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(y0 - RW + j, 0, h - 1) * w * 8));
+    }
+    for (int p = 0; p < nph; ++p) {
+      const int s = s_first + p;
+      if (s < s_end) {
+        const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+        double acc[8];
+        rw_vert_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], win, wp, acc);
+        double* Vs = smem + (p & 1) * kRwStrip;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) Vs[rw_row(t) + c] = acc[t];
+      }
+      lds_barrier();  // strip p written; strip p - 1 read by the consumers
+    }
+    return;
+  }
+  // consumer: horizontal item (k_gauss_rw's lane map over the 256 consumer lanes)
+  float* const L_gauss = L.gauss ? L.gauss + im * L.gauss_bs : nullptr;
+  float* const L_dog = L.dog + im * L.dog_bs;
+  double* const L_next_seed = L.next_seed ? L.next_seed + im * L.seed_bs : nullptr;
+  const int c = threadIdx.x - 256;
+  int hcg, hr0, hr1;
+  {
+    int g, j;
+    b128_group(c & 63, g, j);
+    const int gid = 4 * (c >> 6) + g;
+    hcg = 8 * (gid >> 1) + (j & 7);
+    hr0 = j < 8 ? (gid & 1) : 6 + (gid & 1);
+    hr1 = j < 8 ? 4 + (gid & 1) : 2 + (gid & 1);
+  }
+  const bool hact = hcg < G::NCG;
+  const long long plane = (long long)h * w;
+  const bool st = !(L.dbg & 1);
+  double lprev[2][4];
+  lds_barrier();  // phase 0: the producers write strip 0
+  for (int p = 1; p < nph; ++p) {
+    const int s = s_first + p - 1;
+    if (hact) {
+      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+      const double* Vs = smem + ((p - 1) & 1) * kRwStrip;
+      int hc = hcg, h0 = hr0, h1 = hr1;
+      asm volatile("" : "+v"(hc), "+v"(h0), "+v"(h1));  // per-scale opaque: no hoisted per-radius addresses
+      double o[2][4];
+      rw_horz_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], Vs + rw_row(h0) + 4 * hc,
+                       Vs + rw_row(h1) + 4 * hc, wp, o);
+      const int x = x0 + 4 * hc, nvalid = w - x;
+      const unsigned pb = (unsigned)plane * 4u;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int y = y0 + (i ? h1 : h0);
+        const bool own = y < h && nvalid > 0;
+        double d[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[i][q];
+        if (s >= s_begin && st) {
+          if (L.vec) {
+            const int voff = own ? (y * w + x) * 4 : 0x7ffffff0;  // dropped past the plane
+            if (L_gauss)
+              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000), voff, o[i]);
+            if (s > 0)
+              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000), voff, d);
+          } else if (own) {
+            const long long pp = (long long)y * w + x;
+            if (L_gauss) store4(L_gauss + s * plane + pp, o[i], nvalid);
+            if (s > 0) store4(L_dog + (s - 1) * plane + pp, d, nvalid);
+          }
+        }
+        if (s == P.S && L_next_seed && s >= s_begin && own && !(y & 1)) {
+          double* sd = L_next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+          sd[0] = o[i][0];
+          if (nvalid > 2) sd[1] = o[i][2];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lprev[i][q] = o[i][q];
+      }
+    }
+    lds_barrier();  // strip p - 1 read: the producers may overwrite it in phase p + 1
+  }
+}
+
+// Octaves >= 1 through k_gauss_rw: radii up to 24 (the register window of
+// 8 + 2 RW rows per lane), planes of at least 2 columns (SIFT_RW=0:
+// k_gauss_dog, A/B builds).
+static int rw_width(const Pyramid& P, int o) {
+  const int R = P.oct[o].rmax;
+  return R <= 12 ? 12 : R <= 16 ? 16 : R <= 24 ? 24 : 0;
+}
+
+bool gauss_wide(const Pyramid& P, int o) {
+  static const int on = exp_knob("SIFT_RW", 0);
+  static const int rlim = exp_knob("SIFT_RW_R", 24);
+  return on && o >= 1 && P.oct[o].w >= 2 && P.oct[o].rmax <= std::min(rlim, 24) && rw_width(P, o) > 0 &&
+         !gauss_keep_l64(P, o);
+}
+
+static int rw_tile_w(const Pyramid& P, int o) { return rw_width(P, o) <= 16 ? 224 : 192; }
+static size_t rw_lds(const Pyramid& P, int o) { (void)P; (void)o; return sizeof(double) * 2 * kRwStrip; }
 
 // Materialised octave-0 base (fp64), for octave-0 radii beyond kUR.
 __global__ __launch_bounds__(256) void k_upsample_base(const Pyramid P, double* __restrict__ b) {
@@ -1751,7 +1648,7 @@ bool gauss_keep_l64(const Pyramid& P, int o) {
 // never) run the split vertical pass (k_gauss_vert) before the tile kernel.
 bool gauss_vsplit(const Pyramid& P, int o) {
   static const int rmin = exp_knob("SIFT_VSPLIT_R", 40);
-  return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin;
+  return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin && !gauss_wide(P, o);
 }
 
 static bool staged0(const Pyramid& P, int o) { return o == 0 && !gauss_needs_base0(P); }
@@ -1787,6 +1684,7 @@ static size_t staged_bytes(const Pyramid& P, int o) {
 }
 
 size_t gauss_lds_bytes(const Pyramid& P, int o, bool fused) {
+  if (!fused && gauss_wide(P, o)) return rw_lds(P, o);
   return sizeof(double) * kGY * strip_stride(P, o) + staged_bytes(P, o) +
          (fused ? sizeof(float) * 3 * kRingPlane : 0);
 }
@@ -1873,20 +1771,6 @@ static void set_attr() {
                             160 * 1024);
 }
 
-// LDS-resident path (k_gauss_lds): bytes of the strip (64 rows) + staged
-// region, 0 when octave o does not take it (octave 0, split pass, fp64
-// planes kept, planes narrower than 2 columns, region wider than 128
-// columns, or more than the CU's 160 KiB).  SIFT_GAUSS_LDS=0 turns it off
-// (A/B against k_gauss_dog).
-static size_t lds_path_bytes(const Pyramid& P, int o) {
-  static const int on = exp_knob("SIFT_GAUSS_LDS", 0);
-  if (!on || o == 0 || gauss_vsplit(P, o) || gauss_keep_l64(P, o) || P.oct[o].w < 2) return 0;
-  const int R = P.oct[o].rmax, tw = tile_w(P, o);
-  if (tw + 2 * R > lds_region_stride(tw)) return 0;
-  const size_t b = sizeof(double) * ((size_t)kLY * strip_stride(P, o) + (size_t)(kLY + 2 * R) * lds_region_stride(tw));
-  return b <= 160 * 1024 ? b : 0;
-}
-
 // The base of octave o+1 alone (sift_detect_from_seed_range_device: an
 // octave below the scanned one only feeds its successor).  background.js:
 // 114-118 samples L_o[S] at even rows and columns, so only those values are
@@ -1947,43 +1831,77 @@ hipError_t launch_upsample_base(const Pyramid& P, double* base0, hipStream_t st)
 
 int gauss_tile_rows(const Pyramid& P, int o) { return (P.oct[o].h + kGY - 1) / kGY; }
 
+// Blocks per CU of the octave-o >= 1 launches: the vertical passes re-read
+// the base window of every active block once per scale, and the active
+// blocks of an XCD share its 4 MiB L2.  SIFT_GAUSS_BPC="b1,b2,..." caps the
+// blocks per CU of octaves 1, 2, ... by padding the dynamic LDS
+// (experiments; 0 = no cap).
+static size_t occupancy_lds(int o, size_t lds) {
+  static const std::vector<int> bpc = [] {
+    std::vector<int> v;
+#ifdef SIFT_EXPERIMENTS
+    if (const char* e = std::getenv("SIFT_GAUSS_BPC"))
+      for (const char* p = e; *p;) {
+        v.push_back(std::atoi(p));
+        while (*p && *p != ',') ++p;
+        if (*p) ++p;
+      }
+#endif
+    return v;
+  }();
+  if (o < 1 || o - 1 >= (int)bpc.size() || bpc[o - 1] <= 0) return lds;
+  const size_t cap = (size_t)160 * 1024 / bpc[o - 1] - 1024;
+  return std::max(lds, cap);
+}
+
 hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin, int ty_end) {
   static_assert(kGY == kGaussTileRows, "tile rows");
   const Octave& oc = P.oct[L.o];
   if (L.nimg < 1) L.nimg = 1;
   if (L.fuse && !gauss_can_fuse(P, L.o)) return hipErrorInvalidValue;
   if (L.nimg > 1 && (L.fuse || ty_end >= 0)) return hipErrorInvalidValue;  // batches: whole octaves, no fused decisions
-  if (const size_t lb = ty_end < 0 && !L.fuse && L.nimg == 1 ? lds_path_bytes(P, L.o) : 0) {
-    static bool lattr = false;
-    if (!lattr) {
-      (void)hipFuncSetAttribute((const void*)k_gauss_lds<96, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      (void)hipFuncSetAttribute((const void*)k_gauss_lds<kGX, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      lattr = true;
-    }
-    const int tw = tile_w(P, L.o);
+  if (!L.fuse && !L.vsplit && gauss_wide(P, L.o)) {
+    if (!L.base) return hipErrorInvalidValue;
+    const int RW = rw_width(P, L.o), tw = rw_tile_w(P, L.o);
     L.gx = (oc.w + tw - 1) / tw;
-    L.gy = (oc.h + kLY - 1) / kLY;
-    L.by0 = 0;
-    // one block per CU: split the scales only while the tiles leave CUs idle
+    L.gy = (oc.h + kRwRows - 1) / kRwRows;
+    // Scale groups while the octave has fewer than SIFT_RW_MINB tiles x
+    // groups (each group recomputes the scale before it).
+    static const int minb = exp_knob("SIFT_RW_MINB", 600);
     int G = 1;
-    while (G < P.NS && (long long)L.gx * L.gy * G < 256) ++G;
+    while (G < P.NS && (long long)L.gx * L.gy * G < minb) ++G;
     split_scales(P, L.o, G, L.gb);
     L.G = G;
+    L.by0 = 0;
+    if (ty_end >= 0) {  // a band of kGY-row tile rows: the same rows in 8-row tiles
+      if (ty_begin < 0 || ty_begin >= ty_end) return hipErrorInvalidValue;
+      const int rb = ty_begin * (kGY / kRwRows), re = std::min(L.gy, ty_end * (kGY / kRwRows));
+      if (rb >= re) return hipErrorInvalidValue;
+      L.by0 = rb;
+      L.gy = re - rb;
+    }
     static const int xband = exp_knob("SIFT_XCD_BAND", -1);
     L.xcd_band = (xband >> (L.o - 1)) & 1;
-    L.sw = strip_stride(P, L.o);
+    L.sw = kRwSW;
     static const int dbg = exp_knob("SIFT_GAUSS_DBG", 0);
     L.dbg = dbg;
     const bool a16 = !((reinterpret_cast<uintptr_t>(L.dog)) & 15) &&
-                     (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
+                     (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15)) &&
+                     (L.nimg <= 1 || ((L.dog_bs & 3) == 0 && (!L.gauss || (L.gauss_bs & 3) == 0)));  // every image's planes
     L.vec = (a16 && (oc.w & 3) == 0 && 4.0 * oc.h * oc.w < 2147483648.0) ? 1 : 0;
-    L.zero = oc.rmax > kUR1 ? 1 : 0;
-    if (!L.base) return hipErrorInvalidValue;
-    const dim3 grid(L.gx * L.gy * L.G);
-    if (tw == 96) hipLaunchKernelGGL((k_gauss_lds<96, kUR1>), grid, dim3(512), lb, st, P, L);
-    else hipLaunchKernelGGL((k_gauss_lds<kGX, kUR1>), grid, dim3(512), lb, st, P, L);
+    L.zero = 0;
+    const dim3 grid(L.gx * L.gy * L.G * L.nimg);
+    const size_t lds = occupancy_lds(L.o, rw_lds(P, L.o));
+    static const int pcw = exp_knob("SIFT_PC", 1);  // producer / consumer waves (k_gauss_pc)
+    if (pcw) {
+      if (RW == 12) hipLaunchKernelGGL(k_gauss_pc<12>, grid, dim3(512), lds, st, P, L);
+      else if (RW == 16) hipLaunchKernelGGL(k_gauss_pc<16>, grid, dim3(512), lds, st, P, L);
+      else hipLaunchKernelGGL(k_gauss_pc<24>, grid, dim3(512), lds, st, P, L);
+    } else {
+      if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
+      else if (RW == 16) hipLaunchKernelGGL(k_gauss_rw<16>, grid, dim3(256), lds, st, P, L);
+      else hipLaunchKernelGGL(k_gauss_rw<24>, grid, dim3(256), lds, st, P, L);
+    }
     return hipGetLastError();
   }
   const int G = scale_groups(P, L.o);
@@ -2012,6 +1930,8 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     set_attr<true, kSW0, 8, false>();
     set_attr<true, kSW1, kUR, false>();
     set_attr<false, 0, kUR1, false>();
+    (void)hipFuncSetAttribute((const void*)k_gauss_dog<false, 0, kUR1, false, 96>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     set_attr<true, kSW0, 8, true>();
     set_attr<true, kSW1, kUR, true>();
     attr_set = true;
@@ -2020,7 +1940,8 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
   static const int dbg = exp_knob("SIFT_GAUSS_DBG", 0);
   L.dbg = dbg;
   const bool a16 = !((reinterpret_cast<uintptr_t>(L.dog)) & 15) &&
-                   (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15));
+                   (!L.gauss || !((reinterpret_cast<uintptr_t>(L.gauss)) & 15)) &&
+                   (L.nimg <= 1 || ((L.dog_bs & 3) == 0 && (!L.gauss || (L.gauss_bs & 3) == 0)));  // every image's planes
   L.vec = (a16 && (oc.w & 3) == 0 && 4.0 * oc.h * oc.w < 2147483648.0) ? 1 : 0;
   L.zero = oc.rmax > (staged0(P, L.o) ? kUR : kUR1) ? 1 : 0;
   if (L.vsplit) {
@@ -2028,33 +1949,17 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     hipLaunchKernelGGL(k_gauss_vert, dim3((oc.w + kGX - 1) / kGX, (oc.h + kVertRows - 1) / kVertRows, P.NS * L.nimg),
                        dim3(256), 0, st, P, L.o, L.base, L.vsplit, L.base_bs, L.vsplit_bs);
   }
-  // Producer / consumer waves (k_gauss_ws) for octaves >= 1 whose two
-  // strips fit the CU's LDS (SIFT_GAUSS_WS=0: k_gauss_dog, A/B builds).
-  static const int ws = exp_knob("SIFT_GAUSS_WS", 0);
-  if (ws && L.nimg == 1 && L.o >= 1 && !L.fuse && ty_end < 0 && oc.w >= 2 && 2 * lds <= 160 * 1024) {
-    static bool wattr = false;
-    if (!wattr) {
-      (void)hipFuncSetAttribute((const void*)k_gauss_ws<96, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      (void)hipFuncSetAttribute((const void*)k_gauss_ws<kGX, kUR1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      wattr = true;
-    }
-    if (tw == 96) hipLaunchKernelGGL((k_gauss_ws<96, kUR1>), grid, dim3(512), 2 * lds, st, P, L);
-    else hipLaunchKernelGGL((k_gauss_ws<kGX, kUR1>), grid, dim3(512), 2 * lds, st, P, L);
-    return hipGetLastError();
-  }
   if (L.fuse) {  // staged octave 0 (gauss_can_fuse)
     if (L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, true>), grid, dim3(256), lds, st, P, L);
     else hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, true>), grid, dim3(256), lds, st, P, L);
   } else if (tw == 96) {
-    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false, 96>), grid, dim3(256), lds, st, P, L);
+    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false, 96>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
   } else if (staged0(P, L.o) && L.sw == kSW0) {
     hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, false>), grid, dim3(256), lds, st, P, L);
   } else if (staged0(P, L.o)) {
     hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, false>), grid, dim3(256), lds, st, P, L);
   } else {
-    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false>), grid, dim3(256), lds, st, P, L);
+    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
   }
   return hipGetLastError();
 }

@@ -230,6 +230,8 @@ bool gauss_keep_l64(const Pyramid& P, int o);
 // Octave o runs the split vertical pass (GaussLaunch.vsplit scratch: NS x h x
 // w doubles).
 bool gauss_vsplit(const Pyramid& P, int o);
+// Octave o (>= 1) runs k_gauss_wide (128-column tiles; no split pass).
+bool gauss_wide(const Pyramid& P, int o);
 
 // Fills the unit table of L (octave geometry) and launches the scan; returns
 // the launch error.  L.bitmap words per octave: S * h * nw.
