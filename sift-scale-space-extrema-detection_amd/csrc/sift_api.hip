@@ -125,6 +125,9 @@ struct sift_ctx {
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
   hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
+  // Concurrent octaves (octave_streams): octaves >= 1 on a side stream beside octave 0
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   sift_timings tm{};
   std::vector<double> oct_ms;      // per-octave Gaussian+DoG launch time of the last build
 };
@@ -251,6 +254,9 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   for (auto& e : ctx->ev_go)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_heavy) (void)hipEventDestroy(ctx->ev_heavy);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
   if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -495,8 +501,26 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     ctx->xseed_w = (P.oct[P.O - 1].w + 1) / 2;
     HIPCHK(ctx->xseed.ensure((size_t)ctx->xseed_h * ctx->xseed_w * sizeof(double)));
   }
+  // Octaves >= 1 beside octave 0 (SIFT_OCONC, experiments): the octave-1 base
+  // comes straight from the input (launch_seed0, bit-identical to the
+  // octave-0 launch's seeds), so octaves 1.. run on a side stream while
+  // octave 0 runs on the context's; the pass ends when both have.
+  static const int oconc = exp_knob("SIFT_OCONC", 0);
+  const bool conc = oconc && o_first == 0 && so_end <= o_first && nimg == 1 && !nf && P.O >= 2 &&
+                    !gauss_needs_base0(P) && P.oct[0].rad[P.S] <= 16;
+  if (conc) {
+    if (!ctx->side) {
+      HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    }
+    HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    HIPCHK(launch_seed0(P, ctx->seeds.as<double>() + P.oct[1].seed_off, ctx->side));
+  }
   for (int o = o_first; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
+    hipStream_t ost = conc && o >= 1 ? ctx->side : ctx->stream;
     if (o < so_end) {
       HIPCHK(launch_seed_only(P, o, ctx->seeds.as<double>() + oc.seed_off, ctx->seedv.as<double>(),
                               ctx->seeds.as<double>() + P.oct[o + 1].seed_off, ctx->stream));
@@ -533,9 +557,14 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.base_bs = o == 0 ? 0 : seeds_pi;
     L.l64_bs = P.l64_bstride;
     L.vsplit_bs = ctx->vsplit_pi;
-    HIPCHK(launch_gauss_dog(P, L, ctx->stream));
-    if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
-    HIPCHK(hipEventRecord(ctx->ev_go[o], ctx->stream));
+    if (conc && o == 0) L.next_seed = nullptr;  // launch_seed0 made it
+    HIPCHK(launch_gauss_dog(P, L, ost));
+    if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ost));
+    HIPCHK(hipEventRecord(ctx->ev_go[o], ost));
+  }
+  if (conc) {
+    HIPCHK(hipEventRecord(ctx->ev_join, ctx->side));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
   }
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   ctx->dog_source = kNative;

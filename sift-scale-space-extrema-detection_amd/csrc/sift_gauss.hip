@@ -1321,16 +1321,22 @@ __device__ __forceinline__ void rw_horz(const double* ra, const double* rb, cons
   const cdouble* wq = wp;
 #pragma unroll
   for (int q = 0; q < 4; ++q) out[0][q] = out[1][q] = 0.0;
+  // An odd-D item does not use its first pair's .x: that value is marked used
+  // (empty asm), so every read stays one aligned ds_read_b128 (the compiler
+  // would otherwise drop it and re-pair the reads as 8-byte-aligned
+  // ds_read2_b64s, which conflict).
+  auto rd = [](const double* q) { return *reinterpret_cast<const double2*>(q); };
 #pragma unroll
   for (int n2 = 0; n2 < PF; ++n2) {
-    u[0][n2] = *reinterpret_cast<const double2*>(pa + 2 * n2);
-    u[1][n2] = *reinterpret_cast<const double2*>(pb + 2 * n2);
+    u[0][n2] = rd(pa + 2 * n2);
+    u[1][n2] = rd(pb + 2 * n2);
   }
+  if constexpr (D) asm volatile("" ::"v"(u[0][0].x), "v"(u[1][0].x));
 #pragma unroll
   for (int n2 = 0; n2 < NP; ++n2) {
     if (n2 + PF < NP) {
-      u[0][n2 + PF] = *reinterpret_cast<const double2*>(pa + 2 * (n2 + PF));
-      u[1][n2 + PF] = *reinterpret_cast<const double2*>(pb + 2 * (n2 + PF));
+      u[0][n2 + PF] = rd(pa + 2 * (n2 + PF));
+      u[1][n2 + PF] = rd(pb + 2 * (n2 + PF));
     }
     if (SIFT_RWTAPS > 0 && n2 % (SIFT_RWTAPS > 0 ? SIFT_RWTAPS / 2 : 1) == 0) asm volatile("" : "+s"(wq));
 #pragma unroll
@@ -1364,6 +1370,20 @@ __device__ __forceinline__ void rw_horz_any_(std::integer_sequence<int, Rs...>, 
                                             const double* rb, const cdouble* wp, double (&out)[2][4]) {
   bool done = false;
   ((!done && r == Rs ? (rw_horz<Rs, RW>(ra, rb, wp, out), done = true) : false), ...);
+}
+// ... with the epilogue inside each radius variant (no join of the outputs:
+// the variants' accumulators go straight to their stores).
+template <int RW, class Epi, int... Rs>
+__device__ __forceinline__ void rw_horz_epi_(std::integer_sequence<int, Rs...>, int r, const double* ra,
+                                            const double* rb, const cdouble* wp, Epi&& epi) {
+  bool done = false;
+  ((!done && r == Rs ? ([&] {
+     double o[2][4];
+     rw_horz<Rs, RW>(ra, rb, wp, o);
+     epi(o);
+   }(), done = true)
+                     : false),
+   ...);
 }
 
 template <int RW>
@@ -1483,8 +1503,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
 // consumer wave of the block, so the producer's fmas fill the consumer's
 // LDS and store latency; the two roles run separate loops, so their
 // registers do not add up (the window lives only in the producer's).
+#ifndef SIFT_PC_WPE
+#define SIFT_PC_WPE 1  // minimum waves per SIMD the register allocation must allow (experiments)
+#endif
 template <int RW>
-__global__ __launch_bounds__(512) void k_gauss_pc(const Pyramid P, const GaussLaunch L) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SIFT_PC_WPE))) void k_gauss_pc(const Pyramid P,
+                                                                                                   const GaussLaunch L) {
   using G = RwGeom<RW>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const Octave& oc = P.oct[L.o];
@@ -1512,16 +1536,26 @@ __global__ __launch_bounds__(512) void k_gauss_pc(const Pyramid P, const GaussLa
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
       const int xoff = clampi(x0 - RW + c, 0, w - 1) * 8;
+      if (L.dbg & 8) {  // dbg 8: timing without the window loads
 #pragma unroll
-      for (int j = 0; j < G::NW; ++j)
-        win[j] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(y0 - RW + j, 0, h - 1) * w * 8));
+        for (int j = 0; j < G::NW; ++j) win[j] = (double)(c + j);
+      } else {
+#pragma unroll
+        for (int j = 0; j < G::NW; ++j)
+          win[j] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(y0 - RW + j, 0, h - 1) * w * 8));
+      }
     }
     for (int p = 0; p < nph; ++p) {
       const int s = s_first + p;
       if (s < s_end) {
         const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
         double acc[8];
-        rw_vert_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], win, wp, acc);
+        if (L.dbg & 4) {  // dbg 4: timing without the vertical fmas
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[t] = win[t + RW];
+        } else {
+          rw_vert_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], win, wp, acc);
+        }
         double* Vs = smem + (p & 1) * kRwStrip;
 #pragma unroll
         for (int t = 0; t < 8; ++t) Vs[rw_row(t) + c] = acc[t];
@@ -1556,38 +1590,46 @@ __global__ __launch_bounds__(512) void k_gauss_pc(const Pyramid P, const GaussLa
       const double* Vs = smem + ((p - 1) & 1) * kRwStrip;
       int hc = hcg, h0 = hr0, h1 = hr1;
       asm volatile("" : "+v"(hc), "+v"(h0), "+v"(h1));  // per-scale opaque: no hoisted per-radius addresses
-      double o[2][4];
-      rw_horz_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], Vs + rw_row(h0) + 4 * hc,
-                       Vs + rw_row(h1) + 4 * hc, wp, o);
-      const int x = x0 + 4 * hc, nvalid = w - x;
       const unsigned pb = (unsigned)plane * 4u;
+      auto epi = [&](const double (&o)[2][4]) {
+        const int x = x0 + 4 * hc, nvalid = w - x;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int y = y0 + (i ? h1 : h0);
-        const bool own = y < h && nvalid > 0;
-        double d[4];
+        for (int i = 0; i < 2; ++i) {
+          const int y = y0 + (i ? h1 : h0);
+          const bool own = y < h && nvalid > 0;
+          double d[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[i][q];
-        if (s >= s_begin && st) {
-          if (L.vec) {
-            const int voff = own ? (y * w + x) * 4 : 0x7ffffff0;  // dropped past the plane
-            if (L_gauss)
-              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000), voff, o[i]);
-            if (s > 0)
-              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000), voff, d);
-          } else if (own) {
-            const long long pp = (long long)y * w + x;
-            if (L_gauss) store4(L_gauss + s * plane + pp, o[i], nvalid);
-            if (s > 0) store4(L_dog + (s - 1) * plane + pp, d, nvalid);
+          for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[i][q];
+          if (s >= s_begin && st) {
+            if (L.vec) {
+              const int voff = own ? (y * w + x) * 4 : 0x7ffffff0;  // dropped past the plane
+              if (L_gauss)
+                bstore4(__builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000), voff, o[i]);
+              if (s > 0)
+                bstore4(__builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000), voff, d);
+            } else if (own) {
+              const long long pp = (long long)y * w + x;
+              if (L_gauss) store4(L_gauss + s * plane + pp, o[i], nvalid);
+              if (s > 0) store4(L_dog + (s - 1) * plane + pp, d, nvalid);
+            }
           }
-        }
-        if (s == P.S && L_next_seed && s >= s_begin && own && !(y & 1)) {
-          double* sd = L_next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
-          sd[0] = o[i][0];
-          if (nvalid > 2) sd[1] = o[i][2];
-        }
+          if (s == P.S && L_next_seed && s >= s_begin && own && !(y & 1)) {
+            double* sd = L_next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
+            sd[0] = o[i][0];
+            if (nvalid > 2) sd[1] = o[i][2];
+          }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) lprev[i][q] = o[i][q];
+          for (int q = 0; q < 4; ++q) lprev[i][q] = o[i][q];
+        }
+      };
+      if (L.dbg & 2) {  // dbg 2: timing without the horizontal pass (one strip read per item row)
+        double o[2][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[0][q] = Vs[rw_row(h0) + 4 * hc + q], o[1][q] = Vs[rw_row(h1) + 4 * hc + q];
+        epi(o);
+      } else {
+        rw_horz_epi_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], Vs + rw_row(h0) + 4 * hc,
+                         Vs + rw_row(h1) + 4 * hc, wp, epi);
       }
     }
     lds_barrier();  // strip p - 1 read: the producers may overwrite it in phase p + 1
@@ -1805,6 +1847,61 @@ __global__ __launch_bounds__(256) void k_seed_horz(const Pyramid P, int o, const
   double acc = 0.0;
   for (int i = 0; i <= 2 * r; ++i) acc = __builtin_fma(wt[i], row[clampi(2 * xp + i - r, 0, w - 1)], acc);
   next[(long long)yp * nw + xp] = acc;
+}
+
+// The base of octave 1 straight from the input (the octave-0 launch need not
+// run first): seed[i][j] = L0[S][2i][2j] with octave 0's fma chains --
+// vertical sums of the 2x upsample B[y][x] = I[y >> 1][x >> 1] (clamped),
+// taps in increasing order from 0.0, then horizontal sums -- so the values
+// are bit-identical to the ones the octave-0 kernel writes (the vertical sums
+// depend on x only through x >> 1: one per input column).  A block owns 64
+// seed columns x 8 seed rows: the vertical sums of its 8 rows (upsampled rows
+// 2i) over the input columns the horizontal taps reach go to LDS, then one
+// lane per seed column runs the horizontal sums of the 8 rows.
+constexpr int kS0X = 64, kS0Y = 8;
+__global__ __launch_bounds__(256) void k_seed0(const Pyramid P, double* __restrict__ next, int next_w) {
+  __shared__ double vs[kS0Y][kS0X + 2 * 9 + 2];  // input columns j0 - hr .. j0 + 63 + hr (hr = ceil(r/2) <= 8)
+  const Octave& oc = P.oct[0];
+  const int r = oc.rad[P.S];
+  const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[P.S]);
+  const int h0 = oc.h, w0 = oc.w;  // 2H x 2W
+  const int h1 = P.oct[1].h;
+  const int j0 = blockIdx.x * kS0X, i0 = blockIdx.y * kS0Y;
+  const int hr = (r + 1) >> 1;
+  const int ncol = kS0X + 2 * hr;  // input columns j0 - hr .. j0 + 63 + hr
+  // vertical: item = (seed row t, input column c); B row y - r + k, y = 2 (i0 + t)
+  for (int it = threadIdx.x; it < kS0Y * ncol; it += 256) {
+    const int t = it / ncol, c = it - t * ncol;
+    const int y = 2 * (i0 + t);
+    const int xc = clampi(j0 - hr + c, 0, P.W - 1);  // input column (the upsampled column's x >> 1, clamped)
+    const float* col = P.img + xc;
+    double acc = 0.0;
+    for (int k = 0; k <= 2 * r; ++k)
+      acc = fma((double)wp[k], (double)col[(long long)(clampi(y - r + k, 0, h0 - 1) >> 1) * P.img_stride], acc);
+    vs[t][c] = acc;
+  }
+  __syncthreads();
+  // horizontal: seed (i0 + t, j0 + q), upsampled x = 2 (j0 + q); tap k reads
+  // upsampled column clamp(x - r + k), i.e. input column clamp(..) >> 1
+  const int q = threadIdx.x & 63;
+  const int j = j0 + q, x = 2 * j;
+  for (int t = threadIdx.x >> 6; t < kS0Y; t += 4) {
+    const int i = i0 + t;
+    if (i >= h1 || j >= next_w) continue;
+    double acc = 0.0;
+    for (int k = 0; k <= 2 * r; ++k) {
+      const int xi = clampi(x - r + k, 0, w0 - 1) >> 1;  // input column
+      acc = fma((double)wp[k], vs[t][xi - (j0 - hr)], acc);
+    }
+    next[(long long)i * next_w + j] = acc;
+  }
+}
+
+hipError_t launch_seed0(const Pyramid& P, double* next, hipStream_t st) {
+  if (P.O < 2 || !next || gauss_needs_base0(P) || P.oct[0].rad[P.S] > 16) return hipErrorInvalidValue;
+  const int w1 = P.oct[1].w, h1 = P.oct[1].h;
+  hipLaunchKernelGGL(k_seed0, dim3((w1 + kS0X - 1) / kS0X, (h1 + kS0Y - 1) / kS0Y), dim3(256), 0, st, P, next, w1);
+  return hipGetLastError();
 }
 
 size_t seed_only_scratch(const Pyramid& P, int o) {

@@ -232,6 +232,8 @@ bool gauss_keep_l64(const Pyramid& P, int o);
 bool gauss_vsplit(const Pyramid& P, int o);
 // Octave o (>= 1) runs k_gauss_wide (128-column tiles; no split pass).
 bool gauss_wide(const Pyramid& P, int o);
+// The octave-1 base straight from the input (bit-identical to the octave-0 launch's seeds).
+hipError_t launch_seed0(const Pyramid& P, double* next, hipStream_t st);
 
 // Fills the unit table of L (octave geometry) and launches the scan; returns
 // the launch error.  L.bitmap words per octave: S * h * nw.

@@ -58,16 +58,16 @@ const contexts = new Map();
 function deviceState(device = 0) {
   let st = contexts.get(device);
   if (!st) {
-    // queue: detectAsync jobs of this context run one after another (a native
-    // context is not re-entrant; the addon rejects any call while a job runs).
-    st = { ctx: native.createContext(device), gen: 0, stage: null, W: 0, H: 0, params: null,
-      queue: Promise.resolve() };
+    // pool: detectAsync's contexts (asyncPool; a native context is not
+    // re-entrant, the addon rejects any call on it while its job runs).
+    st = { ctx: native.createContext(device), device, gen: 0, stage: null, W: 0, H: 0, params: null, pool: null };
     contexts.set(device, st);
   }
   return st;
 }
 
 function bump(st, stage, W, H, params) {
+  st.lastCtx = st.ctx;  // lastTimings: the context of the latest call
   st.gen += 1;
   st.stage = stage;
   st.W = W;
@@ -361,6 +361,17 @@ export function refineCandidateKeypoints(args, candidate_keypoints, scales_per_o
   return keypointsFromNative(r);
 }
 
+// Keypoints as the caller asked for them: 'objects' (default: the
+// reference's keypoint objects, background.js:660-671) or 'typed' (no
+// per-keypoint objects: {count, ints, doubles}, ints = [octave, scaleLevel,
+// localX, localY] and doubles = [absoluteSigma, absoluteX, absoluteY,
+// interpolatedValue] per keypoint, in the reference's order).
+function keypointsOut(r, format) {
+  if (format === 'typed') return { count: r.ints.length / 4, ints: r.ints, doubles: r.doubles };
+  if (format !== undefined && format !== 'objects') throw new TypeError(`unknown keypoint format '${format}'`);
+  return keypointsFromNative(r);
+}
+
 function keypointsFromNative(r) {
   const n = r.ints.length / 4;
   const out = new Array(n);
@@ -378,14 +389,14 @@ function keypointsFromNative(r) {
 // One-call fast path: all four stages on device, keypoints out.
 // ---------------------------------------------------------------------------
 export function detect(input_image, { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8,
-  assumed_blur = 0.5, min_interpixel_distance = 0.5, device = 0 } = {}) {
+  assumed_blur = 0.5, min_interpixel_distance = 0.5, device = 0, format } = {}) {
   const img = toGray(input_image);
   const st = deviceState(device);
   const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
   const r = img.rgba ? native.detectRgba(st.ctx, img.data, img.width, img.height, params)
     : native.detect(st.ctx, img.data, img.width, img.height, params);
   bump(st, 'detected', img.width, img.height, params);
-  return keypointsFromNative(r);
+  return keypointsOut(r, format);
 }
 
 // A batch of independent images of one size (BASELINE cfg 4's images per
@@ -393,7 +404,7 @@ export function detect(input_image, { number_of_octaves = 5, scales_per_octave =
 // batch); returns one keypoint list per image, each exactly what detect()
 // returns for that image.
 export function detectBatch(images, { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8,
-  assumed_blur = 0.5, min_interpixel_distance = 0.5, device = 0 } = {}) {
+  assumed_blur = 0.5, min_interpixel_distance = 0.5, device = 0, format } = {}) {
   if (!images.length) return [];
   const grays = images.map(toGray);
   const { width, height } = grays[0];
@@ -407,35 +418,81 @@ export function detectBatch(images, { number_of_octaves = 5, scales_per_octave =
   const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
   const r = native.detectBatch(st.ctx, data, grays.length, width, height, params);
   bump(st, 'detected', width, height, params);
-  const all = keypointsFromNative(r);
   const out = [];
   let at = 0;
+  if (format === 'typed') {
+    for (const c of r.counts) {
+      out.push({ count: c, ints: r.ints.subarray(4 * at, 4 * (at + c)), doubles: r.doubles.subarray(4 * at, 4 * (at + c)) });
+      at += c;
+    }
+    return out;
+  }
+  const all = keypointsOut(r, format);
   for (const c of r.counts) { out.push(all.slice(at, at + c)); at += c; }
   return out;
 }
 
-// Calls on one device are serialised: each job starts when the previous one
-// on that device has settled (Promise.all over many images is fine); a
-// synchronous call on the device while a job runs throws (SIFT_E_BUSY).
+// Asynchronous detections run on a pool of `inflight` contexts per device
+// (default 3; each has its own HIP stream and pyramid), so up to that many
+// images are on the GPU at once and one image's host work (H2D of the
+// input, keypoint copy, result conversion) overlaps the others' device
+// work.  Jobs beyond the pool wait in FIFO order.  The pool's first context
+// is the device's synchronous one: a synchronous call on the device while a
+// job runs on it throws (SIFT_E_BUSY), as before.
+function asyncPool(st, inflight) {
+  if (!st.pool) st.pool = { ctxs: [{ ctx: st.ctx, busy: false }], waiters: [] };
+  const want = Math.max(1, inflight | 0);
+  while (st.pool.ctxs.length < want) st.pool.ctxs.push({ ctx: native.createContext(st.device), busy: false });
+  return st.pool;
+}
+
+function release(pool, slot) {
+  const i = pool.waiters.findIndex((w) => pool.ctxs.indexOf(slot) < w.limit);
+  if (i >= 0) {
+    const [w] = pool.waiters.splice(i, 1);
+    w.resolve(slot);  // handed over still busy
+  } else {
+    slot.busy = false;
+  }
+}
+
 export function detectAsync(input_image, opts = {}) {
   const { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8, assumed_blur = 0.5,
-    min_interpixel_distance = 0.5, device = 0 } = opts;
+    min_interpixel_distance = 0.5, device = 0, inflight = 3, format } = opts;
   const st = deviceState(device);
-  const run = async () => {
-    let img = toGray(input_image);
-    if (img.rgba) img = { width: img.width, height: img.height, data: native.rgbaToGray(st.ctx, img.data, img.width, img.height, false).gray };
-    const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
-    bump(st, 'detecting', img.width, img.height, params);
-    const r = await native.detectAsync(st.ctx, img.data, img.width, img.height, params);
-    return keypointsFromNative(r);
+  const pool = asyncPool(st, inflight);
+  const limit = Math.max(1, inflight | 0);
+  const start = (slot) => {
+    let job;
+    try {
+      let img = toGray(input_image);
+      if (img.rgba) {
+        img = { width: img.width, height: img.height,
+          data: native.rgbaToGray(slot.ctx, img.data, img.width, img.height, false).gray };
+      }
+      const params = nativeParams(number_of_octaves, scales_per_octave, min_blur_level, assumed_blur, min_interpixel_distance);
+      if (slot.ctx === st.ctx) bump(st, 'detecting', img.width, img.height, params);
+      job = native.detectAsync(slot.ctx, img.data, img.width, img.height, params);
+    } catch (e) {
+      release(pool, slot);
+      return Promise.reject(e);
+    }
+    return job.then((r) => {
+      release(pool, slot);
+      st.lastCtx = slot.ctx;
+      return keypointsOut(r, format);
+    }, (e) => {
+      release(pool, slot);
+      throw e;
+    });
   };
-  // An idle device starts the job at once (the native job is queued before
-  // this returns); otherwise it waits for the jobs ahead of it.
-  st.pending = (st.pending || 0) + 1;
-  const job = st.pending === 1 ? run() : st.queue.then(run, run);
-  const done = () => { st.pending -= 1; };
-  st.queue = job.then(done, done);
-  return job;
+  // A free context starts the job before this returns; otherwise it waits.
+  const free = pool.ctxs.slice(0, limit).find((c) => !c.busy);
+  if (free) {
+    free.busy = true;
+    return start(free);
+  }
+  return new Promise((resolve) => pool.waiters.push({ resolve, limit })).then(start);
 }
 
 export function lastCounts(device = 0) {
@@ -446,7 +503,8 @@ export function lastCounts(device = 0) {
 // gaussDogMs, extremaMs, refineMs, h2dMs, gaussOct0Ms) and the host wall
 // time of its last keypoint copy to the host (d2hMs).
 export function lastTimings(device = 0) {
-  return native.timings(deviceState(device).ctx);
+  const st = deviceState(device);
+  return native.timings(st.lastCtx || st.ctx);
 }
 
 // ---------------------------------------------------------------------------

@@ -45,7 +45,8 @@ static napi_value throw_sift(napi_env env, struct sift_ctx *ctx, int rc, const c
 typedef struct {
   struct sift_ctx *ctx;
   int busy;
-  int flags;  /* sift_params.flags of the last build / load through this handle */
+  int flags;       /* sift_params.flags of the last build / load through this handle */
+  double d2h_ms;   /* host wall time of this context's last keypoint copy (JS thread only) */
 } ctx_box;
 
 static void ctx_finalize(napi_env env, void *data, void *hint) {
@@ -403,22 +404,19 @@ static napi_value js_refine_params(napi_env env, napi_callback_info info) {
   return NULL;
 }
 
-/* Host wall time of the last keypoint copy to the host (device->host of the
- * 48-byte records, completed before return), ms: timings().d2hMs. */
-static double g_d2h_ms = 0.0;
-
 static double now_ms(void) {
   struct timespec t;
   clock_gettime(CLOCK_MONOTONIC, &t);
   return (double)t.tv_sec * 1e3 + (double)t.tv_nsec * 1e-6;
 }
 
-/* Copy of the last keypoints to a malloc'd host array (*out; NULL on error). */
-static int copy_keypoints_host(struct sift_ctx *ctx, size_t *n, sift_keypoint **out) {
+/* Copy of the last keypoints to a malloc'd host array (*out; NULL on error);
+ * *ms = host wall time of the device->host copy of the 48-byte records. */
+static int copy_keypoints_host(struct sift_ctx *ctx, size_t *n, sift_keypoint **out, double *ms) {
   sift_keypoint *tmp = (sift_keypoint *)malloc(sizeof(sift_keypoint) * (*n ? *n : 1));
   const double t0 = now_ms();
   int rc = sift_copy_keypoints(ctx, tmp, *n, n);
-  g_d2h_ms = now_ms() - t0;
+  *ms = now_ms() - t0;
   if (rc) {
     free(tmp);
     tmp = NULL;
@@ -453,9 +451,10 @@ static napi_value keypoint_arrays(napi_env env, sift_keypoint *tmp, size_t n, si
   return out;
 }
 
-static napi_value keypoints_to_js(napi_env env, struct sift_ctx *ctx, size_t n, size_t singular) {
+static napi_value keypoints_to_js(napi_env env, ctx_box *box, size_t n, size_t singular) {
+  struct sift_ctx *ctx = box->ctx;
   sift_keypoint *tmp = NULL;
-  int rc = copy_keypoints_host(ctx, &n, &tmp);
+  int rc = copy_keypoints_host(ctx, &n, &tmp, &box->d2h_ms);
   if (rc) return throw_sift(env, ctx, rc, "sift_copy_keypoints");
   return keypoint_arrays(env, tmp, n, singular);
 }
@@ -465,12 +464,14 @@ static napi_value js_refine(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  ctx_box *box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  struct sift_ctx *ctx = box->ctx;
   if (!ctx) return NULL;
   size_t n = 0, sing = 0;
   int rc = sift_refine(ctx, NULL, 0, &n, &sing);
   if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_refine");
-  return keypoints_to_js(env, ctx, n, sing);
+  return keypoints_to_js(env, box, n, sing);
 }
 
 /* detect(ctx, img, width, height, params) -> {ints, doubles, singular} */
@@ -478,7 +479,9 @@ static napi_value js_detect(napi_env env, napi_callback_info info) {
   size_t argc = 5;
   napi_value argv[5];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  ctx_box *box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  struct sift_ctx *ctx = box->ctx;
   if (!ctx) return NULL;
   size_t len = 0;
   const float *img = (const float *)typed_data(env, argv[1], napi_float32_array, &len);
@@ -496,7 +499,7 @@ static napi_value js_detect(napi_env env, napi_callback_info info) {
   if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_detect");
   size_t sing = 0;
   sift_last_counts(ctx, NULL, NULL, NULL, &sing, NULL);
-  return keypoints_to_js(env, ctx, n, sing);
+  return keypoints_to_js(env, box, n, sing);
 }
 
 /* detectBatch(ctx, Float32Array of n images back to back, n, w, h, params) ->
@@ -506,7 +509,9 @@ static napi_value js_detect_batch(napi_env env, napi_callback_info info) {
   size_t argc = 6;
   napi_value argv[6];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  ctx_box *box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  struct sift_ctx *ctx = box->ctx;
   if (!ctx) return NULL;
   size_t len = 0;
   const float *img = (const float *)typed_data(env, argv[1], napi_float32_array, &len);
@@ -525,7 +530,7 @@ static napi_value js_detect_batch(napi_env env, napi_callback_info info) {
   if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_detect_batch");
   size_t sing = 0;
   sift_last_counts(ctx, NULL, NULL, NULL, &sing, NULL);
-  napi_value out = keypoints_to_js(env, ctx, n, sing);
+  napi_value out = keypoints_to_js(env, box, n, sing);
   if (!out) return NULL;
   int nb = 0;
   sift_last_block_counts(ctx, NULL, 0, &nb);
@@ -557,6 +562,7 @@ typedef struct {
   sift_params p;
   size_t n;
   sift_keypoint *kp;  /* host records, copied on the worker thread */
+  double d2h_ms;      /* their copy's wall time, published to the context on the JS thread */
 } detect_job;
 
 static void detect_execute(napi_env env, void *data) {
@@ -564,7 +570,7 @@ static void detect_execute(napi_env env, void *data) {
   detect_job *j = (detect_job *)data;
   j->rc = sift_detect(j->ctx, j->img, j->w, j->h, (size_t)j->w, &j->p, NULL, 0, &j->n);
   if (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR) {
-    const int rc = copy_keypoints_host(j->ctx, &j->n, &j->kp);
+    const int rc = copy_keypoints_host(j->ctx, &j->n, &j->kp, &j->d2h_ms);
     if (rc) j->rc = rc;
   }
 }
@@ -572,6 +578,7 @@ static void detect_execute(napi_env env, void *data) {
 static void detect_complete(napi_env env, napi_status status, void *data) {
   detect_job *j = (detect_job *)data;
   j->box->busy = 0;
+  j->box->d2h_ms = j->d2h_ms;
   if (status == napi_ok && (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR)) {
     size_t sing = 0;
     sift_last_counts(j->ctx, NULL, NULL, NULL, &sing, NULL);
@@ -658,14 +665,15 @@ static napi_value js_timings(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  struct sift_ctx *ctx = get_ctx(env, argv[0]);
-  if (!ctx) return NULL;
+  ctx_box *box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  struct sift_ctx *ctx = box->ctx;
   sift_timings t;
   memset(&t, 0, sizeof t);
   int rc = sift_last_timings(ctx, &t);
   if (rc) return throw_sift(env, ctx, rc, "sift_last_timings");
   const char *names[6] = {"gaussDogMs", "extremaMs", "refineMs", "h2dMs", "gaussOct0Ms", "d2hMs"};
-  const double v[6] = {t.gauss_dog_ms, t.extrema_ms, t.refine_ms, t.h2d_ms, t.gauss_oct0_ms, g_d2h_ms};
+  const double v[6] = {t.gauss_dog_ms, t.extrema_ms, t.refine_ms, t.h2d_ms, t.gauss_oct0_ms, box->d2h_ms};
   napi_value out;
   napi_create_object(env, &out);
   for (int i = 0; i < 6; ++i) {
@@ -751,7 +759,9 @@ static napi_value js_detect_rgba(napi_env env, napi_callback_info info) {
   size_t argc = 5;
   napi_value argv[5];
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  struct sift_ctx *ctx = get_ctx(env, argv[0]);
+  ctx_box *box = get_box(env, argv[0]);
+  if (!box) return NULL;
+  struct sift_ctx *ctx = box->ctx;
   if (!ctx) return NULL;
   int32_t w = 0, h = 0;
   const uint8_t *rgba = rgba_args(env, argv, &w, &h);
@@ -763,7 +773,7 @@ static napi_value js_detect_rgba(napi_env env, napi_callback_info info) {
   if (rc && rc != SIFT_E_SINGULAR) return throw_sift(env, ctx, rc, "sift_detect_rgba");
   size_t sing = 0;
   sift_last_counts(ctx, NULL, NULL, NULL, &sing, NULL);
-  return keypoints_to_js(env, ctx, n, sing);
+  return keypoints_to_js(env, box, n, sing);
 }
 
 /* planeImage(ctx, kind, octave, scale, mode, coefficient) -> Uint8ClampedArray(rows*cols*4) */

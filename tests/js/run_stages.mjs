@@ -86,14 +86,26 @@ if (mode !== 'schedule-only') {
     minBlurLevel: P.min_blur, minInterpixelDistance: P.min_interpixel_distance } });
   out.worker = { types: posted.map(m => m.type), matrix2dRows: ss[0][0].image.length,
     refined: posted[posted.length - 1].refinedKeypoints.length };
-  // two overlapping async jobs on one device run one after the other; a
-  // synchronous call while one runs is rejected, not raced
+  // overlapping async jobs on one device run on its pool of contexts (the
+  // first is the synchronous one: a synchronous call while its job runs is
+  // rejected, not raced); more jobs than contexts wait; inflight 1 runs
+  // them one after the other; the typed format carries the same records
   const aopts = { number_of_octaves: P.num_octaves, scales_per_octave: P.scales_per_octave,
     min_blur_level: P.min_blur, assumed_blur: P.assumed_blur };
-  const jobs = [sift.detectAsync(image, aopts), sift.detectAsync(image, aopts)];
+  const jobs = [sift.detectAsync(image, aopts), sift.detectAsync(image, aopts),
+    sift.detectAsync(image, { ...aopts, format: 'typed' }), sift.detectAsync(image, aopts),
+    sift.detectAsync(image, { ...aopts, inflight: 1 })];
   try { sift.lastCounts(); out.busyCode = null; } catch (e) { out.busyCode = e.code || String(e); }
   Promise.all(jobs).then(ks => {
-    out.detectAsync = ks.map(k => k.length);
+    out.detectAsync = ks.map(k => (k.count !== undefined ? k.count : k.length));
+    const t = ks[2], o = ks[0];
+    out.typedEqual = t.count === o.length && o.every((k, i) => k.octave === t.ints[4 * i]
+      && k.scaleLevel === t.ints[4 * i + 1] && k.localX === t.ints[4 * i + 2] && k.localY === t.ints[4 * i + 3]
+      && k.absoluteSigma === t.doubles[4 * i] && k.absoluteX === t.doubles[4 * i + 1]
+      && k.absoluteY === t.doubles[4 * i + 2] && k.interpolatedValue === t.doubles[4 * i + 3]);
+    const dt = sift.detect(image, { ...aopts, format: 'typed' });
+    out.typedSyncEqual = dt.count === o.length && dt.ints.every((v, i) => v === t.ints[i])
+      && dt.doubles.every((v, i) => v === t.doubles[i]);
     out.countsAfter = sift.lastCounts().keypoints;
     fs.writeFileSync(outPath, JSON.stringify(out));
   });

@@ -150,6 +150,47 @@ def test_foreign_dog_is_exact(gpu_ctx):
     np.testing.assert_allclose(got, out[:, 4:], rtol=1e-14, atol=1e-15)
 
 
+def test_foreign_dog_with_nonfinite_values(gpu_ctx):
+    """A caller DoG holding NaN, +Inf and -Inf (sift_load_dog): the
+    reference's strict comparisons (sift.js:227-256) are false for a NaN
+    centre or neighbour and true for an infinite centre above / below finite
+    neighbours; candidates, low-contrast count and refined keypoints (NaN /
+    Inf propagated by the refinement arithmetic, background.js:468-675) equal
+    the oracle's on the same values."""
+    img = blob_image(200, 150, seed=23)
+    p = sift_amd.make_params(4, 3)
+    op = _oracle_params(p)
+    r = orc.OracleRun(img, op, orc.CONV_SEPARABLE)
+    dog32 = r.dog_flat.astype(np.float32)
+    rng = np.random.default_rng(5)
+    for v, frac in ((np.nan, 0.004), (np.inf, 0.001), (-np.inf, 0.001)):
+        idx = rng.choice(dog32.size, int(frac * dog32.size), replace=False)
+        dog32[idx] = v
+    gpu_ctx.load_dog(dog32, 200, 150, p)
+    cand, low = gpu_ctx.find_extrema()
+    r.dog_flat = dog32.astype(np.float64)
+    import ctypes
+    lowc = ctypes.c_long(0)
+    L = orc.lib()
+    n = L.oracle_find_extrema(ctypes.byref(op), 200, 150, r.dog_flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                              None, None, 0, ctypes.byref(lowc))
+    rec = np.zeros((max(n, 1), 4), dtype=np.int32)
+    val = np.zeros(max(n, 1))
+    L.oracle_find_extrema(ctypes.byref(op), 200, 150, r.dog_flat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                          rec.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                          val.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n, ctypes.byref(lowc))
+    assert np.isinf(val[:n]).any(), "the injected infinities make candidates"
+    ref = np.concatenate([rec[:n], val[:n, None]], axis=1).astype(np.float64)
+    check_candidates(cand, ref, value_rtol=0)
+    assert low == lowc.value
+    kp, sing = gpu_ctx.refine()
+    out, osing = r.refine(rec[:n], val[:n])
+    assert sing == osing
+    assert kp.shape[0] == out.shape[0]
+    got = np.stack([kp["abs_sigma"], kp["abs_x"], kp["abs_y"], kp["interp_value"]], axis=1)
+    np.testing.assert_allclose(got, out[:, 4:], rtol=1e-14, atol=1e-15)  # NaN == NaN
+
+
 def test_foreign_scale_space_dog(gpu_ctx):
     """computeDifferenceOfGaussians on a caller scale space: D = L[s-1]-L[s]."""
     img = blob_image(96, 80, seed=22)

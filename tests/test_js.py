@@ -80,7 +80,8 @@ def test_js_stage_chain_matches_reference(name):
     assert out["detect"] == g.refined.shape[0]
     # detectBatch (one batched detection of the image, its mirror and the image again)
     assert out["batchEqual"] and out["batchCounts"][0] == out["batchCounts"][2] == g.refined.shape[0]
-    assert out["detectAsync"] == [g.refined.shape[0]] * 2  # serialised on the one context
+    assert out["detectAsync"] == [g.refined.shape[0]] * 5  # a pool of contexts, jobs queued past it
+    assert out["typedEqual"] and out["typedSyncEqual"]
     assert out["busyCode"] == "SIFT_E_BUSY"
     assert out["countsAfter"] == g.refined.shape[0]
     w = out["worker"]

@@ -58,8 +58,40 @@ out.detectAsync = {
   queued_images: reps, queued_total_ms: qms, queued_mpix_per_s: reps * mpix / (qms / 1e3),
   d2h_ms: sift.lastTimings().d2hMs,
   what: 'await sift.detectAsync(image): the same call on the libuv pool (keypoint copy on the worker thread); '
-    + 'queued: Promise.all over reps images (jobs of one device run one after another)',
+    + 'queued: Promise.all over reps images (on the device\'s pool of 3 contexts)',
 };
+
+// 2b. the typed result format (no per-keypoint JS objects): synchronous,
+// then queued asynchronously on the device's pool of 3 contexts
+{
+  const topts = { ...opts, format: 'typed' };
+  sift.detect(image, topts);
+  const tw = [];
+  let tk;
+  for (let i = 0; i < reps; i++) {
+    const t0 = performance.now();
+    tk = sift.detect(image, topts);
+    tw.push(performance.now() - t0);
+  }
+  out.detect_typed = {
+    keypoints: tk.count, wall_ms: med(tw), mpix_per_s: mpix / (med(tw) / 1e3),
+    what: "sift.detect(image, {format: 'typed'}) -> {count, ints, doubles}: the same records without JS objects",
+  };
+  const nq = Math.max(3 * reps, 12);
+  for (const [name, o] of [['detectAsync_typed_queued', { ...topts, inflight: 3 }],
+    ['detectAsync_objects_queued', { ...opts, inflight: 3 }],
+    ['detectAsync_typed_queued_inflight1', { ...topts, inflight: 1 }]]) {
+    await Promise.all(Array.from({ length: 3 }, () => sift.detectAsync(image, o)));  // pool warm-up
+    const t0 = performance.now();
+    const rs = await Promise.all(Array.from({ length: nq }, () => sift.detectAsync(image, o)));
+    const ms = performance.now() - t0;
+    out[name] = {
+      keypoints: rs[0].count !== undefined ? rs[0].count : rs[0].length, images: nq, total_ms: ms,
+      ms_per_image: ms / nq, mpix_per_s: nq * mpix / (ms / 1e3),
+      what: `Promise.all over ${nq} detectAsync(image, ${JSON.stringify({ format: o.format || 'objects', inflight: o.inflight })})`,
+    };
+  }
+}
 
 // 3. the reference's four stages on host arrays (ImageData-shaped planes)
 const stages = { gauss: [], dog: [], find: [], refine: [] };
