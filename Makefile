@@ -17,9 +17,6 @@ $(PKG)/build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(PKG)/build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-# The extrema scan's max/min run on finite DoG values: no NaN canonicalisation.
-$(PKG)/build/sift_extrema.o: HIPFLAGS += -fno-honor-nans
-
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 

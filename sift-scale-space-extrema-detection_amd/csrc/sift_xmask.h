@@ -33,10 +33,13 @@ __device__ __forceinline__ float from_right(float v) {
 }
 
 // IEEE 754-2019 maximum / minimum (v_maximum3_f32 / v_minimum3_f32 on
-// gfx950).  fmaxf / fminf lower to v_max_f32 behind a canonicalising
-// v_max_f32 x, x, x of every loaded or DPP-moved operand (sNaN quieting in
-// IEEE mode): 3 extra VALU per plane row.  The planes hold no NaN, and a
-// -0 / +0 choice cannot change a comparison, so the decisions are the same.
+// gfx950): a NaN operand gives NaN, so a NaN neighbour makes every strict
+// comparison of the centre false, as the reference's comparisons do
+// (sift.js:227-256; caller-supplied planes may hold NaN / Inf).  fmaxf /
+// fminf would lower to v_max_f32 behind a canonicalising v_max_f32 x, x, x of
+// every loaded or DPP-moved operand (3 extra VALU per plane row), and
+// -fno-honor-nans would let the compiler turn these into v_max_f32, which
+// drops the NaN (tests/test_gpu_parity.py::test_foreign_dog_with_nonfinite_values).
 __device__ __forceinline__ float fmax2(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ float fmin2(float a, float b) { return __builtin_elementwise_minimum(a, b); }
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmax2(a, fmax2(b, c)); }

@@ -7,7 +7,7 @@ PKG=$R/sift-scale-space-extrema-detection_amd
 OUT=$R/build_var/$1
 mkdir -p $OUT
 for f in sift_gauss sift_extrema sift_refine sift_image sift_api; do
-  X=""; [ $f = sift_extrema ] && X="-fno-honor-nans"
+  X=""
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result $X $2 -c -o $OUT/$f.o $PKG/csrc/$f.hip &
 done
 wait
