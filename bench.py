@@ -518,6 +518,11 @@ def main():
                     "iso_ms": round(iso["extrema_ms"], 5),
                     "iso_frac": round(gbs(B_x, iso["extrema_ms"]) / HBM_PEAK_GBS, 4),
                 },
+                "refine_stage": {
+                    "what": "refinement stage (fast pass from the scan's captured patches / DoG gathers, exact "
+                            "re-decisions, compaction), one image at a time",
+                    "iso_ms": round(iso["refine_ms"], 5),
+                },
             },
             "cpu_baseline": None,
             "cpu_baseline_all_cores": None,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 6
+#define SIFT_ABI_VERSION 7
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -192,6 +192,11 @@ int sift_refine(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_
  * recomputing (cap in records; SIFT_E_CAPACITY if too small). */
 int sift_copy_candidates(struct sift_ctx *ctx, sift_extremum *out, size_t cap, size_t *n_out);
 int sift_copy_keypoints(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, size_t *n_out);
+/* The last keypoints as two field arrays (the JS typed result format):
+ * ints[4i..4i+3] = octave, scale_level, local_x, local_y and reals[4i..4i+3]
+ * = abs_sigma, abs_x, abs_y, interp_value of keypoint i, in the reference's
+ * order (background.js:660-671).  Through the context's pinned staging. */
+int sift_copy_keypoints_soa(struct sift_ctx *ctx, int32_t *ints, double *reals, size_t cap, size_t *n_out);
 
 /* Override the two scalars refineCandidateKeypoints receives in its own
  * message (minBlurLevel, minInterpixelDistance: background.js:460-461,

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sift_hip.h"
@@ -41,6 +42,56 @@ struct DBuf {
   template <class T>
   T* as() const { return reinterpret_cast<T*>(p); }
 };
+
+// Grow-only pinned host buffer (staging of host images and keypoint records).
+struct HBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t need) {
+    if (need <= bytes) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t want = need + need / 4 + 256;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+// Row copy between host buffers on up to `nt` threads (host memory bandwidth
+// of one core is well below what the DMA engines take from pinned memory).
+void par_copy_rows(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows, int nt) {
+  auto part = [&](size_t r0, size_t r1) {
+    for (size_t r = r0; r < r1; ++r)
+      std::memcpy((char*)dst + r * dpitch, (const char*)src + r * spitch, width);
+  };
+  if (nt <= 1 || rows * width < ((size_t)4 << 20)) {
+    part(0, rows);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (rows + nt - 1) / nt;
+  for (int t = 1; t < nt; ++t) {
+    const size_t r0 = std::min(rows, t * per), r1 = std::min(rows, (t + 1) * per);
+    if (r0 < r1) th.emplace_back(part, r0, r1);
+  }
+  part(0, std::min(rows, per));
+  for (auto& x : th) x.join();
+}
+
+int host_threads() {
+  static const int n = [] {
+    const unsigned h = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(4u, h ? h : 1u));
+  }();
+  return n;
+}
 
 double js_round(double x) {
   double f = std::floor(x);
@@ -110,6 +161,9 @@ struct sift_ctx {
   DBuf ambbitmap;                              // ambiguous words (k_exact_words)
   bool x_words = false;                        // this extrema stage lists ambiguous words, not keys
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
+  DBuf patch, wslot, cand_patch;               // first-step patches captured by the scan (ExtremaLaunch.patch)
+  bool x_patch = false;                        // this extrema stage captures patches
+  bool has_patch = false;                      // cand_patch indexes the current slots
   DBuf lowbitmap, lowrowcount, lowrowoff;      // low-contrast list (SIFT_F_LOW_CONTRAST_LIST)
   DBuf low_key, low_val, late_key, late_val;
   DBuf keep, pos;                              // keypoint compaction
@@ -122,6 +176,10 @@ struct sift_ctx {
   unsigned* h_counters = nullptr;              // pinned mirror of counters (+ per-block keypoint counts at kBlk)
   int own_lo = -1, own_hi = -1;                // sift_set_owned_rows
   std::vector<long long> blk_counts;           // kept keypoints per (octave, scale) of the last refinement
+  HBuf himg, hkp;                  // pinned staging: host images in, keypoint records out
+  hipEvent_t ev_himg = nullptr;    // the DMA out of himg is done (himg may be refilled)
+  HBuf hpl;                        // pinned staging of plane reads: two halves, double-buffered
+  hipEvent_t ev_pl[2] = {nullptr, nullptr};
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
   hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
@@ -152,6 +210,41 @@ static int check_params(const sift_params* p) {
   if (p->scales_per_octave < 1 || p->scales_per_octave + 3 > kMaxScales) return SIFT_E_UNSUPPORTED;
   if (!(p->min_blur > 0) || !(p->assumed_blur >= 0) || !(p->min_interpixel_distance > 0)) return SIFT_E_ARG;
   return SIFT_OK;
+}
+
+// Device -> pageable host copy through pinned staging: chunks alternate
+// between the two halves of ctx->hpl, so the DMA of chunk i+1 overlaps the
+// (multi-threaded) host copy of chunk i.  A plain hipMemcpy into pageable
+// memory runs at a fraction of the link rate; this keeps the link busy.
+static hipError_t d2h_staged(sift_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  constexpr size_t kChunk = (size_t)8 << 20;
+  if (bytes < ((size_t)1 << 20)) {  // small: one DMA straight into the destination
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
+  }
+  hipError_t e = ctx->hpl.ensure(2 * kChunk);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i)
+    if (!ctx->ev_pl[i]) e = hipEventCreateWithFlags(&ctx->ev_pl[i], hipEventDisableTiming);
+  if (e != hipSuccess) return e;
+  char* half[2] = {(char*)ctx->hpl.p, (char*)ctx->hpl.p + kChunk};
+  const size_t n = (bytes + kChunk - 1) / kChunk;
+  auto len = [&](size_t i) { return std::min(kChunk, bytes - i * kChunk); };
+  auto issue = [&](size_t i) {
+    hipError_t r = hipMemcpyAsync(half[i & 1], (const char*)src + i * kChunk, len(i), hipMemcpyDeviceToHost,
+                                  ctx->stream);
+    return r != hipSuccess ? r : hipEventRecord(ctx->ev_pl[i & 1], ctx->stream);
+  };
+  for (size_t i = 0; i < std::min<size_t>(n, 2) && e == hipSuccess; ++i) e = issue(i);
+  for (size_t i = 0; i < n && e == hipSuccess; ++i) {
+    e = hipEventSynchronize(ctx->ev_pl[i & 1]);
+    if (e != hipSuccess) break;
+    const size_t piece = 256 << 10, l = len(i), rows = l / piece;  // 256 KB rows split over the threads
+    par_copy_rows((char*)dst + i * kChunk, piece, half[i & 1], piece, piece, rows, host_threads());
+    if (l > rows * piece) std::memcpy((char*)dst + i * kChunk + rows * piece, half[i & 1] + rows * piece, l - rows * piece);
+    if (i + 2 < n) e = issue(i + 2);
+  }
+  if (e != hipSuccess) (void)hipStreamSynchronize(ctx->stream);  // nothing left writing into hpl
+  return e;
 }
 
 extern "C" {
@@ -247,13 +340,19 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab,
                   &ctx->lowbitmap, &ctx->lowrowcount, &ctx->lowrowoff, &ctx->low_key, &ctx->low_val,
                   &ctx->late_key, &ctx->late_val, &ctx->band_cnt, &ctx->band_first, &ctx->band_start,
-                  &ctx->perm};
+                  &ctx->perm, &ctx->patch, &ctx->wslot, &ctx->cand_patch};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->ev_go)
     if (e) (void)hipEventDestroy(e);
   if (ctx->ev_heavy) (void)hipEventDestroy(ctx->ev_heavy);
+  ctx->himg.release();
+  ctx->hkp.release();
+  if (ctx->ev_himg) (void)hipEventDestroy(ctx->ev_himg);
+  ctx->hpl.release();
+  for (auto& e : ctx->ev_pl)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -287,6 +386,9 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
   ctx->p = *p;
   ctx->scan_first = 0;
   ctx->planes_first = 0;
+  ctx->has_patch = false;
+  ctx->P.vsum = nullptr;
+  ctx->P.vsum_oct = -1;
   ctx->W = W;
   ctx->H = H;
   ctx->dims.assign(2 * O, 0);
@@ -446,11 +548,20 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     P.img = nullptr;
     P.img_stride = 0;
   } else if (img_host) {  // (a batch: image b from img_host + b * img_bstride, dense on the device)
-    HIPCHK(ctx->img.ensure((size_t)W * H * nimg * sizeof(float)));
+    // Through the context's pinned staging: the rows are copied on several
+    // host threads, then one DMA (the runtime's pageable path stages them on
+    // one thread).  The staging is refilled only after the previous DMA out
+    // of it has completed.
+    const size_t img_bytes = (size_t)W * H * nimg * sizeof(float);
+    HIPCHK(ctx->img.ensure(img_bytes));
+    if (!ctx->ev_himg) HIPCHK(hipEventCreateWithFlags(&ctx->ev_himg, hipEventDisableTiming));
+    else HIPCHK(hipEventSynchronize(ctx->ev_himg));
+    HIPCHK(ctx->himg.ensure(img_bytes));
     for (int b = 0; b < nimg; ++b)
-      HIPCHK(hipMemcpy2DAsync(ctx->img.as<float>() + (size_t)b * W * H, W * sizeof(float),
-                              img_host + (size_t)b * img_bstride, stride * sizeof(float), W * sizeof(float), H,
-                              hipMemcpyHostToDevice, ctx->stream));
+      par_copy_rows((float*)ctx->himg.p + (size_t)b * W * H, W * sizeof(float), img_host + (size_t)b * img_bstride,
+                    stride * sizeof(float), W * sizeof(float), H, host_threads());
+    HIPCHK(hipMemcpyAsync(ctx->img.p, ctx->himg.p, img_bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_himg, ctx->stream));
     P.img = ctx->img.as<float>();
     P.img_stride = W;
     P.img_bstride = nimg > 1 ? (long long)W * H : 0;
@@ -478,6 +589,14 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     if (sv) HIPCHK(ctx->seedv.ensure(sv * sizeof(double)));
     if (vs) HIPCHK(ctx->vsplit.ensure(vs * nimg * sizeof(double)));
     ctx->vsplit_pi = (long long)vs;
+    // after the pass the scratch holds the last split octave's sums (octaves run in order)
+    P.vsum_oct = -1;
+    for (int o = so_end; o < P.O; ++o)
+      if (gauss_vsplit(P, o)) P.vsum_oct = o;
+    static const int vsum_exact = exp_knob("SIFT_VSUM_EXACT", 1);  // 0: the exact passes recompute (A/B)
+    if (!vsum_exact) P.vsum_oct = -1;
+    P.vsum = P.vsum_oct >= 0 ? ctx->vsplit.as<double>() : nullptr;
+    P.vsum_bstride = ctx->vsplit_pi;
   }
   HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
   const double* base0 = nullptr;
@@ -652,8 +771,7 @@ int sift_get_plane(sift_ctx* ctx, int kind, int o, int s, float* dst, size_t cap
     return set_err(ctx, SIFT_E_ARG, "bad plane kind");
   }
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipMemcpyAsync(dst, src, plane * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(d2h_staged(ctx, dst, src, plane * sizeof(float)));
   return SIFT_OK;
 }
 
@@ -830,6 +948,19 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   }
   L.lowbitmap = ctx->want_low ? ctx->lowbitmap.as<unsigned long long>() : nullptr;
   L.lowrowcount = ctx->want_low ? ctx->lowrowcount.as<unsigned>() : nullptr;
+  // Patch capture (SIFT_PATCH=0: the refinement gathers every step, experiments).
+  static const int capture = exp_knob("SIFT_PATCH", 1);
+  const size_t slots = (size_t)ni * extrema_units(P) * kPatchUnitSlots;
+  // the scan's patch stores take 32-bit byte offsets (a larger batch gathers)
+  ctx->x_patch = SIFT_XPATCH && capture != 0 && slots * kPatchFloats * sizeof(float) < ((size_t)1 << 31);
+  ctx->has_patch = false;
+  if (ctx->x_patch) {
+    HIPCHK(ctx->patch.ensure(std::max<size_t>(slots, 1) * kPatchFloats * sizeof(float)));
+    HIPCHK(ctx->wslot.ensure((size_t)words * sizeof(unsigned)));
+    HIPCHK(ctx->cand_patch.ensure((size_t)ctx->cand_cap * sizeof(unsigned)));
+    L.patch = ctx->patch.as<float>();
+    L.wslot = ctx->wslot.as<unsigned>();
+  }
   return SIFT_OK;
 }
 
@@ -874,6 +1005,11 @@ static int extrema_finish(sift_ctx* ctx) {
     // refinement reads each candidate's plane value from its own patch.
     static const int defer = exp_knob("SIFT_DEFER_VALUES", 1);
     E.deferred = defer != 0;
+    if (ctx->x_patch) {  // the scanned octaves carry captured patches, the fused ones gather
+      E.wslot = ctx->wslot.as<unsigned>();
+      E.cand_patch = ctx->cand_patch.as<unsigned>();
+      for (int o = ctx->x_nf; o < P.O; ++o) E.patch_oct |= 1u << o;
+    }
     HIPCHK(launch_emit(P, E, ctx->stream));
   }
   if (ctx->want_low) {  // the certain low-contrast extrema, in order (same scan + emission as the candidates)
@@ -952,6 +1088,7 @@ static int extrema_finish(sift_ctx* ctx) {
   ctx->slot_cap = (int)ctx->cand_cap;
   ctx->has_keep = true;
   ctx->slots_rows = true;
+  ctx->has_patch = ctx->x_patch;
   ctx->ext_pending = true;
   return SIFT_OK;
 }
@@ -1046,6 +1183,10 @@ static int refine_enqueue(sift_ctx* ctx) {
     R.uncertain = ctx->uncertain.as<unsigned>();
     R.counters = cnt;
     R.perm = nullptr;
+    if (ctx->has_patch && ctx->slots_rows) {
+      R.cand_patch = ctx->cand_patch.as<unsigned>();
+      R.patch = ctx->patch.as<float>();
+    }
     static const int band_order = exp_knob("SIFT_BAND_ORDER", 1);
     // strip order (SIFT_REFINE_STRIP = bitmap words per strip, 0 = whole
     // rows: band order): pieces (octave, band, strip, scale, row)
@@ -1338,6 +1479,7 @@ int sift_set_candidates(sift_ctx* ctx, const sift_extremum* cand, size_t n) {
   ctx->ext_pending = false;
   ctx->has_keep = false;
   ctx->slots_rows = false;
+  ctx->has_patch = false;
   ctx->have_cand = true;
   return SIFT_OK;
 }
@@ -1351,6 +1493,44 @@ int sift_copy_keypoints(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n
     HIPCHK(hipMemcpyAsync(out, ctx->kp.p, ctx->n_kp * sizeof(sift_keypoint), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   }
+  return SIFT_OK;
+}
+
+// The records as two field arrays (one DMA into the context's pinned staging,
+// one pass over it on the host threads).
+int sift_copy_keypoints_soa(sift_ctx* ctx, int32_t* ints, double* reals, size_t cap, size_t* n_out) {
+  if (!ctx) return SIFT_E_ARG;
+  if (n_out) *n_out = ctx->n_kp;
+  if (!ints || !reals) return ints || reals ? SIFT_E_ARG : SIFT_OK;
+  if (cap < ctx->n_kp) return set_err(ctx, SIFT_E_CAPACITY, "keypoint buffer too small");
+  const size_t n = ctx->n_kp;
+  if (!n) return SIFT_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(ctx->hkp.ensure(n * sizeof(sift_keypoint)));
+  HIPCHK(hipMemcpyAsync(ctx->hkp.p, ctx->kp.p, n * sizeof(sift_keypoint), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const sift_keypoint* k = (const sift_keypoint*)ctx->hkp.p;
+  auto part = [&](size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1; ++i) {
+      ints[4 * i] = k[i].octave;
+      ints[4 * i + 1] = k[i].scale_level;
+      ints[4 * i + 2] = k[i].local_x;
+      ints[4 * i + 3] = k[i].local_y;
+      reals[4 * i] = k[i].abs_sigma;
+      reals[4 * i + 1] = k[i].abs_x;
+      reals[4 * i + 2] = k[i].abs_y;
+      reals[4 * i + 3] = k[i].interp_value;
+    }
+  };
+  const int nt = n >= 65536 ? host_threads() : 1;
+  std::vector<std::thread> th;
+  const size_t per = (n + nt - 1) / nt;
+  for (int t = 1; t < nt; ++t) {
+    const size_t i0 = std::min(n, t * per), i1 = std::min(n, (t + 1) * per);
+    if (i0 < i1) th.emplace_back(part, i0, i1);
+  }
+  part(0, std::min(n, per));
+  for (auto& x : th) x.join();
   return SIFT_OK;
 }
 

@@ -65,6 +65,13 @@ struct Pyramid {
   int nimg;
   unsigned kpi;
   long long img_bstride, seed_bstride, dog_bstride, l64_bstride;
+  // The split vertical pass's fp64 scratch (k_gauss_vert) as the pass left
+  // it: the vertical sums of every (scale, row, column) of octave vsum_oct
+  // (the last split octave; -1 = none), image b at b * vsum_bstride.  The
+  // exact passes read their patches' vertical sums from it.
+  const double* vsum;
+  long long vsum_bstride;
+  int vsum_oct;
   Octave oct[kMaxOctaves];
 };
 

@@ -58,6 +58,31 @@ __device__ inline void dog_patch(const Pyramid& P, int im, int o, int s, int y, 
   const int nc0 = 2 * oc.rad[s - 1] + 3, nc1 = 2 * oc.rad[s] + 3, nc2 = 2 * oc.rad[s + 1] + 3,
             nc3 = 2 * oc.rad[s + 2] + 3;
   const int o1 = 3 * nc0, o2 = o1 + 3 * nc1, o3 = o2 + 3 * nc2, o4 = o3 + 3 * nc3;
+  if (P.vsum && o == P.vsum_oct) {
+    // The split pass already formed every vertical sum of this octave (the
+    // same chain, bit for bit): 8 independent loads per lane in flight
+    // instead of 12 (2r+3) chains of 2r+1 dependent steps (4K octave 3:
+    // ~18 rounds of 95 per lane).
+    const double* vb = P.vsum + im * P.vsum_bstride + (long long)(y - 1) * w;
+    const long long plane = (long long)h * w;
+    for (int i0 = lane; i0 < o4; i0 += 8 * NT) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int idx = min(i0 + u * NT, o4 - 1);
+        const int k = idx >= o3 ? 3 : idx >= o2 ? 2 : idx >= o1 ? 1 : 0;
+        const int base = k == 3 ? o3 : k == 2 ? o2 : k == 1 ? o1 : 0;
+        const int nc = k == 3 ? nc3 : k == 2 ? nc2 : k == 1 ? nc1 : nc0;
+        const int t = s - 1 + k, r = oc.rad[t];
+        const int li = idx - base;
+        const int a = li / nc, c = li - nc * a;
+        v[u] = vb[t * plane + (long long)a * w + clampi(x - 1 - r + c, 0, w - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u * NT < o4) sh[i0 + u * NT] = v[u];
+    }
+  } else
   for (int idx = lane; idx < o4; idx += NT) {
     const int k = idx >= o3 ? 3 : idx >= o2 ? 2 : idx >= o1 ? 1 : 0;
     const int base = k == 3 ? o3 : k == 2 ? o2 : k == 1 ? o1 : 0;

@@ -50,6 +50,8 @@ struct XUnit {
   unsigned long long* lowbitmap;  // the same for the certain low-contrast extrema (LOWL)
   unsigned* lowrowcount;
   unsigned low;
+  unsigned pbase, pcount;  // patch capture: the unit's first slot, slots taken
+  __amdgpu_buffer_rsrc_t prsrc;  // the patch buffer (< 4 GiB: extrema_prepare checks)
   long long word0;     // index of (s_first, row 0, word 0) in L.bitmap (ambiguous word list)
 };
 
@@ -62,6 +64,48 @@ __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int
     dst[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                            U.rsrc, (int)U.xoff, (int)(rofs + (unsigned)q * U.plane_bytes),
                                            SIFT_XLOAD_AUX));
+}
+
+// Patch capture of scale q at centre row y (ExtremaLaunch.patch): each
+// candidate's 19 first-step values come from three lanes -- its own column (9
+// values) and the columns left and right of it (5 each) -- all already in the
+// window, so no DPP moves.  The word's candidates take the next slots of the
+// unit (a wave-uniform count: no atomics -- one global counter serialised
+// ~600 K atomics at the L2, 0.42 -> 6.8 ms).  Returns the slot of the first
+// one (~0u: the unit is out of slots, these candidates gather in the refinement).
+template <int NP, int A, int B, int C>
+__device__ __forceinline__ unsigned x_capture(const XWin<NP>& Wn, XUnit<NP>& U, const ExtremaLaunch& L,
+                                              const int Q, unsigned long long b) {
+  const unsigned cnt = (unsigned)__popcll(b);
+  if (U.pcount + cnt > (unsigned)kPatchUnitSlots) return ~0u;
+  const unsigned base = U.pbase + U.pcount;
+  U.pcount += cnt;
+  // Buffer stores of the window registers themselves: the slot's byte offset
+  // in one VGPR, the word's first slot in an SGPR, the field in the
+  // instruction's offset (16-byte or flat stores would copy each quad into
+  // consecutive registers / keep 64-bit addresses: a wave per SIMD less).
+  const int sb = (int)(base * (unsigned)(kPatchFloats * 4));
+  const int lane = U.lane;
+  auto st = [&](float v, int voff, int field) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), U.prsrc, voff + 4 * field, sb, 0);
+  };
+  if ((b >> lane) & 1ull) {  // the candidate's own column: d(k, a, 1)
+    const int vo = (int)lane_prefix(b) * (kPatchFloats * 4);
+    st(Wn.cv[A][Q - 1], vo, 0); st(Wn.cv[B][Q - 1], vo, 1); st(Wn.cv[C][Q - 1], vo, 2);
+    st(Wn.cv[A][Q], vo, 3); st(Wn.cv[B][Q], vo, 4); st(Wn.cv[C][Q], vo, 5);
+    st(Wn.cv[A][Q + 1], vo, 6); st(Wn.cv[B][Q + 1], vo, 7); st(Wn.cv[C][Q + 1], vo, 16);
+  }
+  if (lane < 63 && ((b >> (lane + 1)) & 1ull)) {  // left of a candidate: d(1, a, 0), d(0, 1, 0), d(2, 1, 0)
+    const int vo = (int)lane_prefix(b >> 1) * (kPatchFloats * 4);
+    st(Wn.cv[A][Q], vo, 8); st(Wn.cv[B][Q], vo, 9); st(Wn.cv[C][Q], vo, 10);
+    st(Wn.cv[B][Q - 1], vo, 11); st(Wn.cv[B][Q + 1], vo, 17);
+  }
+  if (lane > 0 && ((b >> (lane - 1)) & 1ull)) {  // right of a candidate: d(1, a, 2), d(0, 1, 2), d(2, 1, 2)
+    const int vo = (int)lane_prefix(b << 1) * (kPatchFloats * 4);
+    st(Wn.cv[A][Q], vo, 12); st(Wn.cv[B][Q], vo, 13); st(Wn.cv[C][Q], vo, 14);
+    st(Wn.cv[B][Q - 1], vo, 15); st(Wn.cv[B][Q + 1], vo, 18);
+  }
+  return base;
 }
 
 // Centre row y (slots A = y-1, B = y, C = y+1): decide every scale of the group.
@@ -85,6 +129,7 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
   unsigned wlo = 0, whi = 0, wcnt = 0;
   unsigned llo = 0, lhi = 0, lcnt = 0;  // LOWL: the low-contrast word
   unsigned alo = 0, ahi = 0;            // the ambiguous word (L.ambbitmap)
+  unsigned wsl = ~0u;                   // lane q-1: patch slot of scale q's first candidate
 #pragma unroll
   for (int q = 1; q <= NP - 2; ++q) {
     const float v = Wn.cv[B][q];
@@ -96,12 +141,17 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     const unsigned long long bit =
         x_row_decide(v, nmax, nmin, U.colmask, L.c_lo, L.c_hi, L.exact_planes != 0, key, &L.counters[0],
                      L.ambbitmap ? nullptr : L.amb_keys, L.amb_cap, U.low, lowmask, ambmask);
+
     if (ambmask && L.ambbitmap && U.lane == q - 1) {
       alo = (unsigned)(ambmask >> 1);
       ahi = (unsigned)(ambmask >> 33);
     }
     if (bit) {
       const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
+      if (SIFT_XPATCH && L.patch) {
+        const unsigned ps = x_capture<NP, A, B, C>(Wn, U, L, q, bit);
+        if (U.lane == q - 1) wsl = ps;
+      }
       if (U.lane == q - 1) {
         wlo = (unsigned)word;
         whi = (unsigned)(word >> 32);
@@ -124,6 +174,7 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
   if (U.lane < NP - 2) {
     const long long r = (long long)U.lane * U.h + y;
     U.bitmap[r * U.nw + U.xw] = ((unsigned long long)whi << 32) | wlo;
+    if (SIFT_XPATCH && L.patch && (wlo | whi)) L.wslot[U.word0 + r * U.nw + U.xw] = wsl;
     if (wcnt) atomicAdd(&U.rowcount[r], wcnt);
     if ((alo | ahi) && L.ambbitmap) {  // an ambiguous word (rare): its bits and its index for k_exact_words
       const long long gw = U.word0 + r * U.nw + U.xw;
@@ -140,8 +191,8 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
 }
 
 template <int NP, bool LOWL>
-__device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int b, int o, int s_first, int xw,
-                                       int y0, int y1) {
+__device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int b, int u, int o, int s_first,
+                                       int xw, int y0, int y1) {
   const Octave& oc = P.oct[o];
   XUnit<NP> U;
   U.plane = (long long)oc.h * oc.w;
@@ -170,6 +221,9 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
     U.lowrowcount = L.lowrowcount + rb;
   }
   U.low = 0;
+  U.pbase = (unsigned)(b * L.units_per_img + u) * (unsigned)kPatchUnitSlots;
+  U.pcount = 0;
+  if (SIFT_XPATCH && L.patch) U.prsrc = __builtin_amdgcn_make_buffer_rsrc(L.patch, 0, -1, 0x00020000);
 
   XWin<NP> Wn;
   {
@@ -238,11 +292,11 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
   const int s_first = 1 + g * per + min(g, rem);
   const int cnt = per + (g < rem ? 1 : 0);
   switch (cnt) {
-    case 1: x_scan<3, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
-    case 2: x_scan<4, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
-    case 3: x_scan<5, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
-    case 4: x_scan<6, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
-    default: x_scan<7, LOWL>(P, L, b, o, s_first, xw, y0, y1); break;
+    case 1: x_scan<3, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
+    case 2: x_scan<4, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
+    case 3: x_scan<5, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
+    case 4: x_scan<6, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
+    default: x_scan<7, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
   }
 }
 
@@ -269,10 +323,13 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
   const float* __restrict__ Dc = P.dog + im * P.dog_bstride + oc.dog_off + s * plane + (long long)y * w;
   const unsigned kbase = (unsigned)im * P.kpi + oc.key_off + (unsigned)(s - 1) * (unsigned)plane + (unsigned)y * (unsigned)w;
   const int nw = E.nw[o];
-  const unsigned long long* bm = E.bitmap + im * E.words_per_img + E.word_off[o] + (long long)row * nw;
+  const long long wrow = im * E.words_per_img + E.word_off[o] + (long long)row * nw;
+  const unsigned long long* bm = E.bitmap + wrow;
+  const bool patched = E.cand_patch && ((E.patch_oct >> o) & 1u);
   for (int xw0 = 0; xw0 < nw; xw0 += 64) {
     const int xw = xw0 + lane;
     unsigned long long word = xw < nw ? bm[xw] : 0ull;
+    unsigned ps = (patched && word) ? E.wslot[wrow + xw] : ~0u;  // patch slot of the word's first candidate
     unsigned c = (unsigned)__popcll(word);
     // inclusive wave scan of c
     unsigned inc = c;
@@ -291,7 +348,9 @@ __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch 
         E.keys[pos] = kbase + (unsigned)x;
         E.value[pos] = E.deferred ? __builtin_bit_cast(double, 0x7ff8000000000000ull) : (double)Dc[x];
         if (E.keep) E.keep[pos] = 1u;
+        if (E.cand_patch) E.cand_patch[pos] = ps;
       }
+      if (ps != ~0u) ++ps;
       ++pos;
     }
     base += __shfl(inc, 63);
@@ -523,17 +582,28 @@ hipError_t launch_exact_words(const Pyramid& P, ExactLaunch X, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, int o_begin, int o_end) {
-  L.n_oct = P.O;
-  L.ng = (P.S + kXMaxGroup - 1) / kXMaxGroup;
+static int extrema_unit_table(const Pyramid& P, int* unit_off, int* nw) {
+  const int ng = (P.S + kXMaxGroup - 1) / kXMaxGroup;
   int units = 0;
   for (int o = 0; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
-    L.unit_off[o] = units;
-    L.nw[o] = extrema_words_per_row(oc.w);
-    if (oc.h >= 3 && oc.w >= 3 && P.S >= 1) units += L.ng * L.nw[o] * ((oc.h - 2 + kXRows - 1) / kXRows);
+    unit_off[o] = units;
+    nw[o] = extrema_words_per_row(oc.w);
+    if (oc.h >= 3 && oc.w >= 3 && P.S >= 1) units += ng * nw[o] * ((oc.h - 2 + kXRows - 1) / kXRows);
   }
-  L.unit_off[P.O] = units;
+  unit_off[P.O] = units;
+  return units;
+}
+
+int extrema_units(const Pyramid& P) {
+  int uo[kMaxOctaves + 1], nw[kMaxOctaves];
+  return extrema_unit_table(P, uo, nw);
+}
+
+hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, int o_begin, int o_end) {
+  L.n_oct = P.O;
+  L.ng = (P.S + kXMaxGroup - 1) / kXMaxGroup;
+  L.units_per_img = extrema_unit_table(P, L.unit_off, L.nw);
   L.u_begin = L.unit_off[o_begin];
   L.u_end = L.unit_off[o_end];
   if (L.u_end <= L.u_begin) return hipSuccess;

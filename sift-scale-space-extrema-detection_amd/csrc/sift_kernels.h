@@ -95,8 +95,38 @@ struct ExtremaLaunch {
   // layout as bitmap) and lists the word's index (into bitmap) in amb_keys
   // (counters[kAmbWords] of them); k_exact_words re-decides a whole word.
   unsigned long long* ambbitmap;
+  // Patch capture (patch != nullptr): for every candidate bit the scan writes
+  // the 19 fp32 DoG values of its first refinement step (kPatchFloats per
+  // candidate) into its unit's kPatchUnitSlots slots -- unit (image b, u) owns
+  // slots [(b * units_per_img + u) * kPatchUnitSlots, ...), taken in scan
+  // order with a wave-uniform counter, no atomics -- and, for each non-zero
+  // bitmap word, the slot of its first candidate to wslot (same index as
+  // bitmap; ~0u: no patch, the unit's slots ran out: those candidates gather).
+  float* patch;
+  unsigned* wslot;
+  int units_per_img;
 };
 constexpr int kAmbWords = 8;     // counters slot: listed ambiguous words
+#ifndef SIFT_PATCH_SLOTS
+#define SIFT_PATCH_SLOTS 96
+#endif
+constexpr int kPatchUnitSlots = SIFT_PATCH_SLOTS;  // patch slots per scan unit (4K octave 0: ~40 candidates on average)
+// Scan units per image (one wave each: octave, strip of kXRows rows, word, scale group).
+int extrema_units(const Pyramid& P);
+// Patch capture is built only into A/B libraries (-DSIFT_XPATCH=1): 4K
+// extrema stage 0.40 -> 0.50 ms (148 instead of 111 VGPRs: 3 waves per SIMD;
+// 19 dword stores per candidate) for a refinement stage 0.33 -> 0.27 ms,
+// pipelined 7.10 -> 6.54 Gpix/s (profiles/r4p_patch_capture_ab.txt).
+#ifndef SIFT_XPATCH
+#define SIFT_XPATCH 0
+#endif
+// Captured patch of a candidate at (s, y, x), d(k, a, c) = D_{s-1+k}(y-1+a, x-1+c):
+//   [0..8]   d(k, a, 1) at 3k + a (centre column, all three scales and rows) -- except d(2, 2, 1) at [16]
+//   [8..11]  d(1, 0, 0), d(1, 1, 0), d(1, 2, 0), d(0, 1, 0)   (left column)
+//   [12..15] d(1, 0, 2), d(1, 1, 2), d(1, 2, 2), d(0, 1, 2)   (right column)
+//   [16..19] d(2, 2, 1), d(2, 1, 0), d(2, 1, 2), unused
+// Five 16-byte pieces: the centre lane writes 2 + 1, each side lane 1 + 1.
+constexpr int kPatchFloats = 20;
 
 // One launch over every octave: global row g (one wave each) = row_off[o] +
 // (s-1) h_o + y.
@@ -117,6 +147,12 @@ struct EmitLaunch {
   int deferred;                  // 1: value = NaN ("the fp32 plane value"): the refinement reads it from its
                                  // patch, launch_fill_values before the list is copied out; no plane gather here
   long long words_per_img;       // batch: bitmap words per image (rows per image = row_off[n_oct])
+  // Patch indices (cand_patch != nullptr): cand_patch[pos] = wslot of the
+  // word + the bit's rank in it for octaves in patch_oct (scanned with patch
+  // capture), ~0u elsewhere.
+  const unsigned* wslot;
+  unsigned* cand_patch;
+  unsigned patch_oct;
 };
 
 // Fills the deferred (NaN) candidate values of slots [0, *n) from the DoG planes.
@@ -163,6 +199,8 @@ struct RefineLaunch {
   unsigned* counters; // [3] n uncertain, [4] n singular
   const unsigned* perm; // processing order: thread t refines slot perm[t] (nullptr = slot t)
   int wide_exact;       // k_refine_exact: 256 threads per patch (latency) instead of one wave (throughput)
+  const unsigned* cand_patch;  // per slot: captured first-step patch (ExtremaLaunch.patch), ~0u = gather; nullptr = none
+  const float* patch;
 };
 
 // Processing order of the fast refinement (band_order): the slots of the

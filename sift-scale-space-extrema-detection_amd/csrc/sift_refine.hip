@@ -286,13 +286,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int h = oc.h, w = oc.w;
     const long long plane = (long long)h * w;
     const float* __restrict__ D = P.dog + im * P.dog_bstride + oc.dog_off;
+    // the first step's patch as captured by the scan (kPatchFloats layout), if any
+    const unsigned pidx = L.cand_patch ? L.cand_patch[i] : ~0u;
+    const float* __restrict__ pp = L.patch + (size_t)(pidx == ~0u ? 0u : pidx) * kPatchFloats;
     double value = L.cand_val[i];
-    if (value != value) value = (double)D[s * plane + (long long)m * w + n];  // deferred: the fp32 plane value
+    if (value != value)  // deferred: the fp32 plane value
+      value = pidx != ~0u ? (double)pp[4] : (double)D[s * plane + (long long)m * w + n];
     const double dval = EXACT ? 0.0 : fabs(value) * 0x1p-24;
     int status = kRefDiscard;
     double d[27];
     for (int it = 0; it < 5; ++it) {
       double mx = 0;
+      if (it == 0 && pidx != ~0u) {
+        const float4 c0 = *reinterpret_cast<const float4*>(pp), c1 = *reinterpret_cast<const float4*>(pp + 4);
+        const float4 lf = *reinterpret_cast<const float4*>(pp + 8), rt = *reinterpret_cast<const float4*>(pp + 12);
+        const float4 ex = *reinterpret_cast<const float4*>(pp + 16);
+        const float v19[19] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, ex.x,  // d(k, a, 1), 3k + a
+                               lf.x, lf.y, lf.z, lf.w, ex.y, rt.x, rt.y, rt.z, rt.w, ex.z};
+        constexpr int at[19] = {1, 4, 7, 10, 13, 16, 19, 22, 25, 9, 12, 15, 3, 21, 11, 14, 17, 5, 23};
+#pragma unroll
+        for (int j = 0; j < 27; ++j) d[j] = 0.0;
+#pragma unroll
+        for (int j = 0; j < 19; ++j) {
+          d[at[j]] = (double)v19[j];
+          mx = fmax(mx, fabs((double)v19[j]));
+        }
+      } else {
 #pragma unroll
       for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -310,6 +329,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             d[k * 9 + a * 3 + c] = v;
             mx = fmax(mx, fabs(v));
           }
+      }
       // fp32 rounding of the fp64 value (<= |v| 2^-24) plus fp64 noise vs the reference.
       const double delta = EXACT ? 0.0 : mx * (0x1p-24 + 0x1p-40);
       const StepOut R = refine_step<!EXACT>(d, o, s, m, n, value, delta, dval, P.S, P.ND, h, w, P.thr, it == 4,

@@ -53,7 +53,7 @@ template <int NP>
 struct XWin {
   float hx[3][NP], hn[3][NP];  // 3-wide max / min of a row
   float ex[3][NP], en[3][NP];  // 2-wide (x-1, x+1) max / min (centre planes)
-  float cv[3][NP];             // the value (centre planes)
+  float cv[3][NP];             // the value (every plane: the outer ones feed the patch capture)
   float raw[3][NP];            // loaded, not yet derived rows
 };
 
@@ -72,10 +72,10 @@ __device__ __forceinline__ void x_derive(XWin<NP>& Wn, const float (&src)[NP]) {
     const float m2 = fmax2(l, r), n2 = fmin2(l, r);
     Wn.hx[K][q] = fmax2(m2, v);
     Wn.hn[K][q] = fmin2(n2, v);
+    Wn.cv[K][q] = v;
     if (q >= 1 && q <= NP - 2) {
       Wn.ex[K][q] = m2;
       Wn.en[K][q] = n2;
-      Wn.cv[K][q] = v;
     }
   }
 }

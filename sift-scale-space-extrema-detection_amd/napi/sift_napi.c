@@ -12,6 +12,8 @@
  */
 #define NAPI_VERSION 6
 #include <node_api.h>
+#include <pthread.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -137,6 +139,90 @@ static napi_value make_typed(napi_env env, napi_typedarray_type t, size_t n, siz
   return arr;
 }
 
+/* Recycled host buffers for large results (planes, typed keypoint fields).
+ * A fresh ArrayBuffer's pages fault on first touch: 10-19 GB/s into fresh
+ * pages however many threads copy, against 56 GB/s of DMA into touched pages
+ * (profiles/r4p_d2h_probe.txt).  Buffers of >= 1 MiB are external
+ * ArrayBuffers that go back to this pool when V8 collects them (the sizes
+ * recur: one geometry's planes and keypoint counts), so their pages stay
+ * mapped; the external-memory accounting tells V8 to collect.  Finalizers run
+ * on their environment's JS thread, detectAsync takes buffers on the libuv
+ * pool: one lock. */
+#define POOL_MIN_BYTES ((size_t)1 << 20)
+#define POOL_SLOTS 512
+static struct {
+  void *p;
+  size_t bytes;
+} g_pool[POOL_SLOTS];
+static int g_pool_n = 0;
+static size_t g_pool_bytes = 0;
+static const size_t g_pool_cap = (size_t)8 << 30; /* bytes kept for reuse */
+static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static void *pool_take(size_t bytes) {
+  if (bytes >= POOL_MIN_BYTES) {
+    pthread_mutex_lock(&g_pool_mu);
+    for (int i = g_pool_n - 1; i >= 0; --i)
+      if (g_pool[i].bytes == bytes) {
+        void *p = g_pool[i].p;
+        g_pool[i] = g_pool[--g_pool_n];
+        g_pool_bytes -= bytes;
+        pthread_mutex_unlock(&g_pool_mu);
+        return p;
+      }
+    pthread_mutex_unlock(&g_pool_mu);
+  }
+  void *p = NULL;
+  return posix_memalign(&p, 4096, bytes ? bytes : 1) ? NULL : p;
+}
+
+static void pool_give(void *p, size_t bytes) {
+  if (!p) return;
+  if (bytes >= POOL_MIN_BYTES) {
+    pthread_mutex_lock(&g_pool_mu);
+    if (g_pool_n < POOL_SLOTS && g_pool_bytes + bytes <= g_pool_cap) {
+      g_pool[g_pool_n].p = p;
+      g_pool[g_pool_n].bytes = bytes;
+      g_pool_n++;
+      g_pool_bytes += bytes;
+      p = NULL;
+    }
+    pthread_mutex_unlock(&g_pool_mu);
+  }
+  free(p);
+}
+
+static void pool_finalize(napi_env env, void *data, void *hint) {
+  const size_t bytes = (size_t)(uintptr_t)hint;
+  int64_t adj;
+  napi_adjust_external_memory(env, -(int64_t)bytes, &adj);
+  pool_give(data, bytes);
+}
+
+/* An external ArrayBuffer over a pool buffer (takes ownership of p, also on failure). */
+static napi_value pool_arraybuffer(napi_env env, void *p, size_t bytes) {
+  napi_value ab;
+  if (napi_create_external_arraybuffer(env, p, bytes, pool_finalize, (void *)(uintptr_t)bytes, &ab) != napi_ok) {
+    pool_give(p, bytes);
+    return NULL;
+  }
+  int64_t adj;
+  napi_adjust_external_memory(env, (int64_t)bytes, &adj);
+  return ab;
+}
+
+/* make_typed over a recycled buffer (large results). */
+static napi_value make_typed_pooled(napi_env env, napi_typedarray_type t, size_t n, size_t elem, void **data) {
+  const size_t bytes = n * elem;
+  if (bytes < POOL_MIN_BYTES) return make_typed(env, t, n, elem, data);
+  void *p = pool_take(bytes);
+  if (!p) return NULL;
+  napi_value ab = pool_arraybuffer(env, p, bytes), arr;
+  if (!ab || napi_create_typedarray(env, t, n, ab, 0, &arr) != napi_ok) return NULL;
+  if (data) *data = p;
+  return arr;
+}
+
 /* createContext(device) -> external */
 static napi_value js_create_context(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -223,7 +309,8 @@ static napi_value js_get_plane(napi_env env, napi_callback_info info) {
   int rc = sift_get_dims(ctx, o, &rows, &cols);
   if (rc) return throw_sift(env, ctx, rc, "sift_get_dims");
   float *dst;
-  napi_value arr = make_typed(env, napi_float32_array, (size_t)rows * cols, 4, (void **)&dst);
+  napi_value arr = make_typed_pooled(env, napi_float32_array, (size_t)rows * cols, 4, (void **)&dst);
+  if (!arr) return throw_sift(env, ctx, SIFT_E_ARG, "plane buffer allocation");
   rc = sift_get_plane(ctx, kind, o, s, dst, (size_t)rows * cols);
   if (rc) return throw_sift(env, ctx, rc, "sift_get_plane");
   return arr;
@@ -410,38 +497,48 @@ static double now_ms(void) {
   return (double)t.tv_sec * 1e3 + (double)t.tv_nsec * 1e-6;
 }
 
-/* Copy of the last keypoints to a malloc'd host array (*out; NULL on error);
- * *ms = host wall time of the device->host copy of the 48-byte records. */
-static int copy_keypoints_host(struct sift_ctx *ctx, size_t *n, sift_keypoint **out, double *ms) {
-  sift_keypoint *tmp = (sift_keypoint *)malloc(sizeof(sift_keypoint) * (*n ? *n : 1));
+/* The last keypoints as two malloc'd field arrays (sift_copy_keypoints_soa:
+ * one DMA into the context's pinned staging, one host pass); *ms = host wall
+ * time of that copy.  On error both are NULL. */
+typedef struct {
+  int32_t *ints;
+  double *reals;
+  size_t n;
+} kp_soa;
+
+static int copy_keypoints_host(struct sift_ctx *ctx, size_t n, kp_soa *out, double *ms) {
+  out->n = n;
+  out->ints = (int32_t *)pool_take(sizeof(int32_t) * 4 * (n ? n : 1));
+  out->reals = (double *)pool_take(sizeof(double) * 4 * (n ? n : 1));
   const double t0 = now_ms();
-  int rc = sift_copy_keypoints(ctx, tmp, *n, n);
+  int rc = (out->ints && out->reals) ? sift_copy_keypoints_soa(ctx, out->ints, out->reals, n, &out->n) : SIFT_E_ARG;
   *ms = now_ms() - t0;
   if (rc) {
-    free(tmp);
-    tmp = NULL;
+    pool_give(out->ints, sizeof(int32_t) * 4 * (n ? n : 1));
+    pool_give(out->reals, sizeof(double) * 4 * (n ? n : 1));
+    out->ints = NULL;
+    out->reals = NULL;
   }
-  *out = tmp;
+  out->n = n;  /* the buffers' size (sift_copy_keypoints_soa returns the same count) */
   return rc;
 }
 
-/* JS arrays from host keypoint records (takes ownership of tmp). */
-static napi_value keypoint_arrays(napi_env env, sift_keypoint *tmp, size_t n, size_t singular) {
-  int32_t *ints;
-  double *d;
-  napi_value ia = make_typed(env, napi_int32_array, 4 * n, 4, (void **)&ints);
-  napi_value da = make_typed(env, napi_float64_array, 4 * n, 8, (void **)&d);
-  for (size_t i = 0; i < n; ++i) {
-    ints[4 * i] = tmp[i].octave;
-    ints[4 * i + 1] = tmp[i].scale_level;
-    ints[4 * i + 2] = tmp[i].local_x;
-    ints[4 * i + 3] = tmp[i].local_y;
-    d[4 * i] = tmp[i].abs_sigma;
-    d[4 * i + 1] = tmp[i].abs_x;
-    d[4 * i + 2] = tmp[i].abs_y;
-    d[4 * i + 3] = tmp[i].interp_value;
+/* JS typed arrays over the field arrays (external pool buffers: no copy; takes ownership). */
+static napi_value keypoint_arrays(napi_env env, kp_soa *k, size_t singular) {
+  napi_value iab, dab, ia, da;
+  const size_t n = k->n;
+  iab = pool_arraybuffer(env, k->ints, sizeof(int32_t) * 4 * (n ? n : 1));
+  k->ints = NULL;  /* owned by the array buffer (or released) now */
+  if (!iab) {
+    pool_give(k->reals, sizeof(double) * 4 * (n ? n : 1));
+    k->reals = NULL;
+    return NULL;
   }
-  free(tmp);
+  dab = pool_arraybuffer(env, k->reals, sizeof(double) * 4 * (n ? n : 1));
+  k->reals = NULL;
+  if (!dab) return NULL;
+  napi_create_typedarray(env, napi_int32_array, 4 * n, iab, 0, &ia);
+  napi_create_typedarray(env, napi_float64_array, 4 * n, dab, 0, &da);
   napi_value out, sv;
   napi_create_object(env, &out);
   napi_set_named_property(env, out, "ints", ia);      /* octave, scaleLevel, localX, localY */
@@ -452,11 +549,10 @@ static napi_value keypoint_arrays(napi_env env, sift_keypoint *tmp, size_t n, si
 }
 
 static napi_value keypoints_to_js(napi_env env, ctx_box *box, size_t n, size_t singular) {
-  struct sift_ctx *ctx = box->ctx;
-  sift_keypoint *tmp = NULL;
-  int rc = copy_keypoints_host(ctx, &n, &tmp, &box->d2h_ms);
-  if (rc) return throw_sift(env, ctx, rc, "sift_copy_keypoints");
-  return keypoint_arrays(env, tmp, n, singular);
+  kp_soa k;
+  int rc = copy_keypoints_host(box->ctx, n, &k, &box->d2h_ms);
+  if (rc) return throw_sift(env, box->ctx, rc, "sift_copy_keypoints_soa");
+  return keypoint_arrays(env, &k, singular);
 }
 
 /* refine(ctx) -> {ints, doubles, singular} (singular > 0: caller mirrors the reference's TypeError) */
@@ -561,7 +657,7 @@ typedef struct {
   int w, h, rc;
   sift_params p;
   size_t n;
-  sift_keypoint *kp;  /* host records, copied on the worker thread */
+  kp_soa kp;          /* host field arrays, copied on the worker thread */
   double d2h_ms;      /* their copy's wall time, published to the context on the JS thread */
 } detect_job;
 
@@ -570,7 +666,7 @@ static void detect_execute(napi_env env, void *data) {
   detect_job *j = (detect_job *)data;
   j->rc = sift_detect(j->ctx, j->img, j->w, j->h, (size_t)j->w, &j->p, NULL, 0, &j->n);
   if (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR) {
-    const int rc = copy_keypoints_host(j->ctx, &j->n, &j->kp, &j->d2h_ms);
+    const int rc = copy_keypoints_host(j->ctx, j->n, &j->kp, &j->d2h_ms);
     if (rc) j->rc = rc;
   }
 }
@@ -582,8 +678,7 @@ static void detect_complete(napi_env env, napi_status status, void *data) {
   if (status == napi_ok && (j->rc == SIFT_OK || j->rc == SIFT_E_SINGULAR)) {
     size_t sing = 0;
     sift_last_counts(j->ctx, NULL, NULL, NULL, &sing, NULL);
-    napi_value res = keypoint_arrays(env, j->kp, j->n, sing);
-    j->kp = NULL;
+    napi_value res = keypoint_arrays(env, &j->kp, sing);
     if (res) {
       napi_resolve_deferred(env, j->deferred, res);
     } else {
@@ -599,7 +694,8 @@ static void detect_complete(napi_env env, napi_status status, void *data) {
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, j->deferred, err);
   }
-  free(j->kp);
+  free(j->kp.ints);
+  free(j->kp.reals);
   napi_delete_reference(env, j->img_ref);
   napi_delete_reference(env, j->ctx_ref);
   napi_delete_async_work(env, j->work);

@@ -46,7 +46,7 @@ ABI_SYMBOLS = (
     "sift_last_error", "sift_schedule", "sift_octave_dims", "sift_build_scale_space",
     "sift_build_scale_space_device", "sift_get_dims", "sift_get_blur_level", "sift_get_plane",
     "sift_load_dog", "sift_load_scale_space", "sift_find_extrema", "sift_refine",
-    "sift_set_candidates", "sift_refine_params", "sift_copy_candidates", "sift_copy_keypoints",
+    "sift_set_candidates", "sift_refine_params", "sift_copy_candidates", "sift_copy_keypoints", "sift_copy_keypoints_soa",
     "sift_copy_keypoints_device", "sift_detect", "sift_detect_device", "sift_last_counts",
     "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
     "sift_detect_device_async", "sift_detect_wait", "sift_ctx_create_shared",
@@ -146,6 +146,7 @@ def lib():
         "sift_copy_low_contrast": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_set_flags": (ctypes.c_int, [vp, ctypes.c_int]),
         "sift_copy_keypoints": (ctypes.c_int, [vp, vp, sz, szp]),
+        "sift_copy_keypoints_soa": (ctypes.c_int, [vp, vp, vp, sz, szp]),
         "sift_copy_keypoints_device": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_detect": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_detect_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
@@ -356,6 +357,19 @@ class Context:
         self._check(self._L.sift_copy_keypoints(self._h, out.ctypes.data_as(ctypes.c_void_p), out.shape[0],
                                                 ctypes.byref(n)), "sift_copy_keypoints")
         return out[:n.value]
+
+    def keypoints_soa(self):
+        """The last keypoints as (ints int32 [n, 4]: octave, scale_level,
+        local_x, local_y; reals float64 [n, 4]: abs_sigma, abs_x, abs_y,
+        interp_value) -- sift_copy_keypoints_soa, the JS typed format."""
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_copy_keypoints_soa(self._h, None, None, 0, ctypes.byref(n)), "sift_copy_keypoints_soa")
+        ints = np.zeros((max(n.value, 1), 4), dtype=np.int32)
+        reals = np.zeros((max(n.value, 1), 4), dtype=np.float64)
+        self._check(self._L.sift_copy_keypoints_soa(self._h, ints.ctypes.data_as(ctypes.c_void_p),
+                                                    reals.ctypes.data_as(ctypes.c_void_p), ints.shape[0],
+                                                    ctypes.byref(n)), "sift_copy_keypoints_soa")
+        return ints[:n.value], reals[:n.value]
 
     def refine_params(self, min_blur_level, min_interpixel_distance=0.5):
         self._check(self._L.sift_refine_params(self._h, float(min_blur_level), float(min_interpixel_distance)),

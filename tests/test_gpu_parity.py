@@ -117,6 +117,26 @@ def test_low_contrast_list_stage_api_and_flags(gpu_ctx):
     check_candidates(lc2, orc.as_records(lrec, lval))
 
 
+def test_plane_reads_through_staging_round_trip(gpu_ctx):
+    """sift_get_plane copies through double-buffered pinned staging in 8 MB
+    chunks: a loaded DoG pyramid reads back bit-exact, for a plane of 3.15
+    chunks (ragged last chunk) and for sub-megabyte planes (direct copy)."""
+    W, H = 1500, 1100
+    p = sift_amd.make_params(4, 3)
+    px = [a * b for a, b in orc.octave_dims(W, H, 4)]
+    rng = np.random.default_rng(5)
+    dog = rng.standard_normal(sum(px) * 5).astype(np.float32)
+    gpu_ctx.load_dog(dog, W, H, p)
+    assert px[0] * 4 > 3 * (8 << 20)
+    off = 0
+    for o in range(4):
+        h, w = gpu_ctx.dims(o)
+        assert h * w == px[o]
+        for s in range(5):
+            np.testing.assert_array_equal(gpu_ctx.plane(sift_amd.PLANE_DOG, o, s).ravel(), dog[off:off + h * w])
+            off += h * w
+
+
 def test_foreign_dog_is_exact(gpu_ctx):
     """findCandidateKeypoints / refineCandidateKeypoints on a DoG pyramid the
     context did not build: the fp32 planes are the data, results are exact."""
@@ -189,6 +209,25 @@ def test_foreign_dog_with_nonfinite_values(gpu_ctx):
     assert kp.shape[0] == out.shape[0]
     got = np.stack([kp["abs_sigma"], kp["abs_x"], kp["abs_y"], kp["interp_value"]], axis=1)
     np.testing.assert_allclose(got, out[:, 4:], rtol=1e-14, atol=1e-15)  # NaN == NaN
+
+
+def test_keypoint_field_arrays_equal_records(gpu_ctx):
+    """sift_copy_keypoints_soa (pinned staging, the JS typed format) carries
+    the 48-byte records' fields in order; a host image goes through the
+    context's pinned staging (parallel row copies) and gives the device
+    image's keypoints."""
+    img = blob_image(1024, 600, seed=31)
+    p = sift_amd.make_params(4, 3)
+    gpu_ctx.detect(np.ascontiguousarray(img), p)
+    kp = gpu_ctx.keypoints()
+    ints, reals = gpu_ctx.keypoints_soa()
+    assert ints.shape[0] == kp.shape[0] > 100
+    np.testing.assert_array_equal(ints, np.stack([kp["octave"], kp["scale_level"], kp["local_x"], kp["local_y"]], 1))
+    np.testing.assert_array_equal(reals, np.stack([kp["abs_sigma"], kp["abs_x"], kp["abs_y"], kp["interp_value"]], 1))
+    import torch
+    d_img = torch.from_numpy(np.ascontiguousarray(img)).to("cuda")
+    gpu_ctx.detect_device(d_img.data_ptr(), 1024, 600, p)
+    assert gpu_ctx.keypoints().tobytes() == kp.tobytes()
 
 
 def test_foreign_scale_space_dog(gpu_ctx):
@@ -623,6 +662,40 @@ def test_batch_equals_single_detections(gpu_ctx, W, H, O, S, n):
     # a single image through the batch entry point is the plain detection
     assert gpu_ctx.detect_batch_device(d[n - 1].data_ptr(), 1, W, H, p) == counts[-1]
     assert gpu_ctx.keypoints().tobytes() == singles[-1].tobytes()
+
+
+@pytest.mark.timeout(300)
+def test_batch_mixing_saturated_and_blob_images(gpu_ctx):
+    """Saturated images (whole rows of tied fp32 DoG values: many listed
+    ambiguous words, re-decided by k_exact_words with image-aware keys and
+    row offsets) at batch positions 1 and 3 between blob images: the batch
+    equals the per-image detections byte for byte, and the ambiguous work
+    of images >= 1 is the sum of theirs."""
+    import torch
+    W, H, O, S = 640, 480, 4, 3
+    p = sift_amd.make_params(O, S)
+    imgs = []
+    for i in range(4):
+        img = blob_image(W, H, seed=300 + i)
+        if i % 2:
+            img = (np.clip(np.rint((img - 0.5) * 3.0 * 4096 + 2048), 0, 4096) / 4096).astype(np.float32)
+            assert (img == 0).mean() + (img == 1).mean() > 0.02
+        imgs.append(img)
+    d = torch.from_numpy(np.stack(imgs)).to("cuda:0")
+    singles, exact = [], []
+    for i in range(4):
+        gpu_ctx.detect_device(d[i].data_ptr(), W, H, p)
+        singles.append(gpu_ctx.keypoints().copy())
+        exact.append(gpu_ctx.counts()["exact"])
+    assert exact[1] > 1000 and exact[3] > 1000, exact
+    total = gpu_ctx.detect_batch_device(d.data_ptr(), 4, W, H, p)
+    assert total == sum(s.shape[0] for s in singles)
+    np.testing.assert_array_equal(gpu_ctx.batch_counts(4), [s.shape[0] for s in singles])
+    assert gpu_ctx.keypoints().tobytes() == np.concatenate(singles).tobytes()
+    assert gpu_ctx.counts()["exact"] == sum(exact)
+    # saturated image first: image 0 owns the ambiguous words, then a blob
+    total = gpu_ctx.detect_batch_device(d[1:3].data_ptr(), 2, W, H, p)
+    assert gpu_ctx.keypoints().tobytes() == np.concatenate(singles[1:3]).tobytes()
 
 
 def test_batch_async_and_padded_image_stride(gpu_ctx):

@@ -13,6 +13,6 @@ for r in $(seq $reps); do
   for e in "$@"; do
     i=$((i+1)); [ "$e" = "-" ] && e=""
     env $e timeout -k 10 200 python bench.py --steps ${STEPS:-200} --warmup 10 --no-cpu-baseline --sustain-s 0 ${BENCH_ARGS:-} > $O/ab_$i.json 2> $O/ab_$i.err || { echo "setting '$e' failed"; tail -5 $O/ab_$i.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$O/ab_$i.json')); r=d['roofline']; print('[$e]', d['value'], d['ms_per_step'], 'pass', r['launch_ms'], round(r['frac'],3), [round(o['iso_ms'],4) for o in r['per_octave']], 'x', r['extrema_stage']['iso_ms'])"
+    python3 -c "import json; d=json.load(open('$O/ab_$i.json')); r=d['roofline']; print('[$e]', d['value'], d['ms_per_step'], 'pass', r['launch_ms'], round(r['frac'],3), [round(o['iso_ms'],4) for o in r['per_octave']], 'x', r['extrema_stage']['iso_ms'], 'r', r.get('refine_stage',{}).get('iso_ms'), 'kp', d['keypoints'])"
   done
 done

@@ -116,11 +116,12 @@ for (let i = 0; i < Math.max(2, Math.min(reps, 5)); i++) {
   nk = ref.length;
   stages.extrema_device_ms = ext;
 }
-let planeBytes = 0;
+let planeBytes = 0, dogBytes = 0;
 {
   const dims = [];
   for (let o = 0, h = 2 * H, w = 2 * W; o < O; o++, h = Math.ceil(h / 2), w = Math.ceil(w / 2)) dims.push(h * w);
   planeBytes = dims.reduce((a, p) => a + 4 * p * (2 * S + 5), 0);
+  dogBytes = dims.reduce((a, p) => a + 4 * p * (S + 2), 0);
 }
 const sum = med(stages.gauss) + med(stages.dog) + med(stages.find) + med(stages.refine);
 out.stages = {
@@ -129,6 +130,8 @@ out.stages = {
   findCandidateKeypoints_ms: med(stages.find), refineCandidateKeypoints_ms: med(stages.refine),
   extrema_device_ms: stages.extrema_device_ms, total_ms: sum, mpix_per_s: mpix / (sum / 1e3),
   planes_to_host_bytes: planeBytes,
+  // the DoG stage is pure plane reads (pyramid resident): sift_get_plane into fresh Float32Arrays
+  dog_stage_read_gb_per_s: dogBytes / (med(stages.dog) / 1e3) / 1e9,
   what: 'the reference chain main.js -> worker stages: every Gaussian and DoG plane comes back to the host as an '
     + 'ImageData-shaped Float32Array (the reference returns them), candidates and keypoints as JS objects; '
     + 'the device pyramid stays resident between stages',
