@@ -1494,159 +1494,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
   }
 }
 
-// Producer / consumer form of k_gauss_rw (k_gauss_pc): a block of 8 waves
-// (2 per SIMD); waves 0-3 hold the register windows and run the vertical
-// passes (register fmas only) into one of two strips, waves 4-7 run the
-// horizontal passes and the stores of the previous scale from the other:
-//   phase p:  V(s0 + p) -> strip p % 2   |   H(s0 + p - 1) <- strip (p - 1) % 2
-// one block barrier per phase.  Each SIMD holds one producer and one
-// consumer wave of the block, so the producer's fmas fill the consumer's
-// LDS and store latency; the two roles run separate loops, so their
-// registers do not add up (the window lives only in the producer's).
-#ifndef SIFT_PC_WPE
-#define SIFT_PC_WPE 1  // minimum waves per SIMD the register allocation must allow (experiments)
-#endif
-template <int RW>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SIFT_PC_WPE))) void k_gauss_pc(const Pyramid P,
-                                                                                                   const GaussLaunch L) {
-  using G = RwGeom<RW>;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const Octave& oc = P.oct[L.o];
-  int lb = blockIdx.x;
-  const int bpi = L.gx * L.gy * L.G;
-  if (L.xcd_band) {
-    const int nb = bpi * L.nimg, q = nb >> 3, rm = nb & 7, xc = lb & 7;
-    lb = xc * q + min(xc, rm) + (lb >> 3);
-  }
-  const int im = lb / bpi;
-  lb -= im * bpi;
-  const int bz = lb % L.G, bt = lb / L.G;
-  const int bx = bt % L.gx, by = bt / L.gx + L.by0;
-  const int h = oc.h, w = oc.w;
-  const int x0 = bx * G::TW, y0 = by * kRwRows;
-  const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
-  const int s_first = max(0, s_begin - 1);
-  const int nph = s_end - s_first + 1;  // phases
-  if (threadIdx.x < 256) {
-    // producer: strip column c, window rows y0 - RW .. y0 + 7 + RW of image column x0 - RW + c
-    const int c = threadIdx.x;
-    const double* const L_base = L.base + im * L.base_bs;
-    double win[G::NW];
-    {
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
-      const int xoff = clampi(x0 - RW + c, 0, w - 1) * 8;
-      if (L.dbg & 8) {  // dbg 8: timing without the window loads
-#pragma unroll
-        for (int j = 0; j < G::NW; ++j) win[j] = (double)(c + j);
-      } else {
-#pragma unroll
-        for (int j = 0; j < G::NW; ++j)
-          win[j] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(y0 - RW + j, 0, h - 1) * w * 8));
-      }
-    }
-    for (int p = 0; p < nph; ++p) {
-      const int s = s_first + p;
-      if (s < s_end) {
-        const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
-        double acc[8];
-        if (L.dbg & 4) {  // dbg 4: timing without the vertical fmas
-#pragma unroll
-          for (int t = 0; t < 8; ++t) acc[t] = win[t + RW];
-        } else {
-          rw_vert_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], win, wp, acc);
-        }
-        double* Vs = smem + (p & 1) * kRwStrip;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) Vs[rw_row(t) + c] = acc[t];
-      }
-      lds_barrier();  // strip p written; strip p - 1 read by the consumers
-    }
-    return;
-  }
-  // consumer: horizontal item (k_gauss_rw's lane map over the 256 consumer lanes)
-  float* const L_gauss = L.gauss ? L.gauss + im * L.gauss_bs : nullptr;
-  float* const L_dog = L.dog + im * L.dog_bs;
-  double* const L_next_seed = L.next_seed ? L.next_seed + im * L.seed_bs : nullptr;
-  const int c = threadIdx.x - 256;
-  int hcg, hr0, hr1;
-  {
-    int g, j;
-    b128_group(c & 63, g, j);
-    const int gid = 4 * (c >> 6) + g;
-    hcg = 8 * (gid >> 1) + (j & 7);
-    hr0 = j < 8 ? (gid & 1) : 6 + (gid & 1);
-    hr1 = j < 8 ? 4 + (gid & 1) : 2 + (gid & 1);
-  }
-  const bool hact = hcg < G::NCG;
-  const long long plane = (long long)h * w;
-  const bool st = !(L.dbg & 1);
-  double lprev[2][4];
-  lds_barrier();  // phase 0: the producers write strip 0
-  for (int p = 1; p < nph; ++p) {
-    const int s = s_first + p - 1;
-    if (hact) {
-      const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
-      const double* Vs = smem + ((p - 1) & 1) * kRwStrip;
-      int hc = hcg, h0 = hr0, h1 = hr1;
-      asm volatile("" : "+v"(hc), "+v"(h0), "+v"(h1));  // per-scale opaque: no hoisted per-radius addresses
-      const unsigned pb = (unsigned)plane * 4u;
-      auto epi = [&](const double (&o)[2][4]) {
-        const int x = x0 + 4 * hc, nvalid = w - x;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int y = y0 + (i ? h1 : h0);
-          const bool own = y < h && nvalid > 0;
-          double d[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[i][q];
-          if (s >= s_begin && st) {
-            if (L.vec) {
-              const int voff = own ? (y * w + x) * 4 : 0x7ffffff0;  // dropped past the plane
-              if (L_gauss)
-                bstore4(__builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000), voff, o[i]);
-              if (s > 0)
-                bstore4(__builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000), voff, d);
-            } else if (own) {
-              const long long pp = (long long)y * w + x;
-              if (L_gauss) store4(L_gauss + s * plane + pp, o[i], nvalid);
-              if (s > 0) store4(L_dog + (s - 1) * plane + pp, d, nvalid);
-            }
-          }
-          if (s == P.S && L_next_seed && s >= s_begin && own && !(y & 1)) {
-            double* sd = L_next_seed + (long long)(y >> 1) * L.next_w + (x >> 1);
-            sd[0] = o[i][0];
-            if (nvalid > 2) sd[1] = o[i][2];
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) lprev[i][q] = o[i][q];
-        }
-      };
-      if (L.dbg & 2) {  // dbg 2: timing without the horizontal pass (one strip read per item row)
-        double o[2][4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[0][q] = Vs[rw_row(h0) + 4 * hc + q], o[1][q] = Vs[rw_row(h1) + 4 * hc + q];
-        epi(o);
-      } else {
-        rw_horz_epi_<RW>(std::make_integer_sequence<int, RW + 1>{}, oc.rad[s], Vs + rw_row(h0) + 4 * hc,
-                         Vs + rw_row(h1) + 4 * hc, wp, epi);
-      }
-    }
-    lds_barrier();  // strip p - 1 read: the producers may overwrite it in phase p + 1
-  }
-}
-
-// Octaves >= 1 through k_gauss_rw: radii up to 24 (the register window of
-// 8 + 2 RW rows per lane), planes of at least 2 columns (SIFT_RW=0:
-// k_gauss_dog, A/B builds).
+// Octaves >= 1 through k_gauss_rw: radii up to SIFT_RW_R (the register
+// window of 8 + 2 RW rows per lane; default 12: octave 1 at 4K and 1080p,
+// 0.172 -> 0.158 ms at 4K; RW 24 for octave 2 measured slower, 0.097 ->
+// 0.100 ms: profiles/r4r_register_window_ab.txt), planes of at least 2
+// columns (SIFT_RW=0: k_gauss_dog, A/B builds).
 static int rw_width(const Pyramid& P, int o) {
   const int R = P.oct[o].rmax;
   return R <= 12 ? 12 : R <= 16 ? 16 : R <= 24 ? 24 : 0;
 }
 
 bool gauss_wide(const Pyramid& P, int o) {
-  static const int on = exp_knob("SIFT_RW", 0);
-  static const int rlim = exp_knob("SIFT_RW_R", 24);
+  static const int on = exp_knob("SIFT_RW", 1);
+  static const int rlim = exp_knob("SIFT_RW_R", 12);
   return on && o >= 1 && P.oct[o].w >= 2 && P.oct[o].rmax <= std::min(rlim, 24) && rw_width(P, o) > 0 &&
          !gauss_keep_l64(P, o);
 }
@@ -1989,16 +1849,9 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     L.zero = 0;
     const dim3 grid(L.gx * L.gy * L.G * L.nimg);
     const size_t lds = occupancy_lds(L.o, rw_lds(P, L.o));
-    static const int pcw = exp_knob("SIFT_PC", 1);  // producer / consumer waves (k_gauss_pc)
-    if (pcw) {
-      if (RW == 12) hipLaunchKernelGGL(k_gauss_pc<12>, grid, dim3(512), lds, st, P, L);
-      else if (RW == 16) hipLaunchKernelGGL(k_gauss_pc<16>, grid, dim3(512), lds, st, P, L);
-      else hipLaunchKernelGGL(k_gauss_pc<24>, grid, dim3(512), lds, st, P, L);
-    } else {
-      if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
-      else if (RW == 16) hipLaunchKernelGGL(k_gauss_rw<16>, grid, dim3(256), lds, st, P, L);
-      else hipLaunchKernelGGL(k_gauss_rw<24>, grid, dim3(256), lds, st, P, L);
-    }
+    if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
+    else if (RW == 16) hipLaunchKernelGGL(k_gauss_rw<16>, grid, dim3(256), lds, st, P, L);
+    else hipLaunchKernelGGL(k_gauss_rw<24>, grid, dim3(256), lds, st, P, L);
     return hipGetLastError();
   }
   const int G = scale_groups(P, L.o);

@@ -268,7 +268,7 @@ bool gauss_keep_l64(const Pyramid& P, int o);
 // Octave o runs the split vertical pass (GaussLaunch.vsplit scratch: NS x h x
 // w doubles).
 bool gauss_vsplit(const Pyramid& P, int o);
-// Octave o (>= 1) runs k_gauss_wide (128-column tiles; no split pass).
+// Octave o (>= 1) runs k_gauss_rw (register-window tiles, 224 columns x 8 rows; no split pass).
 bool gauss_wide(const Pyramid& P, int o);
 // The octave-1 base straight from the input (bit-identical to the octave-0 launch's seeds).
 hipError_t launch_seed0(const Pyramid& P, double* next, hipStream_t st);

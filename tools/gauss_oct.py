@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-octave average duration of k_gauss_dog launches in rocprofv3
+"""Per-octave average duration of the Gaussian+DoG launches (k_gauss_dog, k_gauss_rw, k_gauss_vert) in rocprofv3
 kernel_trace.csv files (octave = the launch's tile grid, Grid_Size_X x _Y):
 tools/gauss_oct.py <csv>...  (one column per file), plus k_extrema / k_refine_fast."""
 import csv
@@ -13,8 +13,9 @@ for path in sys.argv[1:]:
     for r in csv.DictReader(open(path)):
         n = r["Kernel_Name"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if "k_gauss_dog" in n:
-            k = "gauss grid %sx%s" % (int(r["Grid_Size_X"]) // 256, r["Grid_Size_Y"])
+        if "k_gauss_dog" in n or "k_gauss_rw" in n or "k_gauss_vert" in n:
+            k = "%s grid %sx%s" % (n.split("(")[0].split("::")[-1].split("<")[0], int(r["Grid_Size_X"]) // 256,
+                                   r["Grid_Size_Y"])
         elif "k_extrema" in n or "k_refine_fast" in n or "k_emit" in n:
             k = n.split("(")[0].split("::")[-1]
         else:

@@ -1,0 +1,10 @@
+#!/bin/bash
+# k_gauss_rw horizontal taps from LDS (SIFT_RW_LT) vs scalar loads: parity subset under the knob, then A/B.
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R || exit 1
+export SIFT_HIP_LIB=$R/build_var/exp.so
+SIFT_RW=1 SIFT_RW_R=24 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  -k "planes_bit_exact or large_radii or batch or row_band or degenerate or unaligned or cfg5_radii or detect_matches_reference or range_detection" \
+  > $O/pytest_r4u.log 2>&1 || { grep -E "PASS|FAIL|Error|passed|failed" $O/pytest_r4u.log | tail -30; exit 1; }
+tail -n 1 $O/pytest_r4u.log
+L0=$R/build_var/lt0.so; L3=$R/build_var/lt3.so
+STEPS=40 timeout -k 10 900 bash tools/gpu_ab_oct.sh 2 SIFT_RW=0 "SIFT_RW=1 SIFT_RW_R=12 SIFT_HIP_LIB=$L0" "SIFT_RW=1 SIFT_RW_R=12" "SIFT_RW=1 SIFT_RW_R=12 SIFT_HIP_LIB=$L3" "SIFT_RW=1 SIFT_RW_R=24" "SIFT_RW=1 SIFT_RW_R=24 SIFT_HIP_LIB=$L3" "SIFT_RS=1 SIFT_RS_BLOCKS=1024"
