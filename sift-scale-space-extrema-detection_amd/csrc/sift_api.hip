@@ -910,15 +910,15 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
     HIPCHK(ctx->low_val.ensure((size_t)ctx->low_cap * sizeof(double)));
     HIPCHK(ctx->late_key.ensure((size_t)ctx->amb_cap * sizeof(unsigned)));
     HIPCHK(ctx->late_val.ensure((size_t)ctx->amb_cap * sizeof(double)));
-    HIPCHK(hipMemsetAsync(ctx->lowrowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), st));
   }
   // fp32 contrast thresholds: rounding is monotone, so |v32| < c_lo proves
   // |v64| < pix_thr and |v32| >= c_hi proves |v64| >= pix_thr.
   const float t_dn = round_toward(P.pix_thr, -1), t_up = round_toward(P.pix_thr, +1);
   // extrema and refinement counters and the refinement's per-block counts: one fill
-  HIPCHK(hipMemsetAsync(cnt, 0, kCntAll * sizeof(unsigned), st));
+  // (+ the row counts, and the low-contrast row counts when listed): one launch
+  HIPCHK(launch_zero_words(cnt, kCntAll, ctx->rowcount.as<unsigned>(), rows + 1,
+                           ctx->want_low ? ctx->lowrowcount.as<unsigned>() : nullptr, rows + 1, st));
   ctx->counters_zeroed = true;
-  HIPCHK(hipMemsetAsync(ctx->rowcount.p, 0, (size_t)(rows + 1) * sizeof(unsigned), st));
   ExtremaLaunch& L = ctx->xl;
   const long long wpi = L.words_per_img;
   const int rpi = L.rows_per_img;
@@ -980,10 +980,10 @@ static int extrema_finish(sift_ctx* ctx) {
   tb = ctx->temp.bytes;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, ctx->rowcount.as<unsigned>(), ctx->rowoff.as<unsigned>(),
                                           (int)(rows + 1), ctx->stream));
-  HIPCHK(hipMemcpyAsync(cnt + kCntN, ctx->rowoff.as<unsigned>() + rows, sizeof(unsigned), hipMemcpyDeviceToDevice,
-                        ctx->stream));
   {
     EmitLaunch E{};
+    E.n_out = cnt + kCntN;  // the list's length, written by k_emit (no 4-byte copy launch)
+    E.n_index = rows;
     E.n_oct = P.O;
     for (int o = 0; o < P.O; ++o) {
       E.row_off[o] = (int)ctx->x_row_off[o];
@@ -1020,9 +1020,9 @@ static int extrema_finish(sift_ctx* ctx) {
     lb = ctx->temp.bytes;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, lb, ctx->lowrowcount.as<unsigned>(),
                                             ctx->lowrowoff.as<unsigned>(), (int)(rows + 1), ctx->stream));
-    HIPCHK(hipMemcpyAsync(cnt + kCntLowSure, ctx->lowrowoff.as<unsigned>() + rows, sizeof(unsigned),
-                          hipMemcpyDeviceToDevice, ctx->stream));
     EmitLaunch E{};
+    E.n_out = cnt + kCntLowSure;
+    E.n_index = rows;
     E.n_oct = P.O;
     for (int o = 0; o < P.O; ++o) {
       E.row_off[o] = (int)ctx->x_row_off[o];

@@ -304,6 +304,7 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
 // order at the row's offset.  Candidate values are the fp32 plane values
 // (ambiguous ones get their exact fp64 value from k_exact_extrema).
 __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch E) {
+  if (E.n_out && blockIdx.x == 0 && threadIdx.x == 0) *E.n_out = E.rowoff[E.n_index];
   const int lane = threadIdx.x & 63;
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row (image-major)
   const int rpi = E.row_off[E.n_oct];
@@ -633,8 +634,29 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
 
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st) {
   const int rows = E.row_off[E.n_oct] * std::max(1, P.nimg);
-  if (rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_emit, dim3((rows + 3) / 4), dim3(256), 0, st, P, E);
+  hipLaunchKernelGGL(k_emit, dim3(std::max(1, (rows + 3) / 4)), dim3(256), 0, st, P, E);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_zero_words(unsigned* a, long long na, unsigned* b, long long nb,
+                                                    unsigned* c, long long nc) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb + nc; i += stride) {
+    if (i < na) a[i] = 0u;
+    else if (i < na + nb) b[i - na] = 0u;
+    else c[i - na - nb] = 0u;
+  }
+}
+
+hipError_t launch_zero_words(unsigned* a, long long na, unsigned* b, long long nb, unsigned* c, long long nc,
+                             hipStream_t st) {
+  if (!a) na = 0;
+  if (!b) nb = 0;
+  if (!c) nc = 0;
+  const long long n = na + nb + nc;
+  if (n <= 0) return hipSuccess;
+  const int grid = (int)std::min<long long>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_zero_words, dim3(grid), dim3(256), 0, st, a, na, b, nb, c, nc);
   return hipGetLastError();
 }
 

@@ -153,6 +153,8 @@ struct EmitLaunch {
   const unsigned* wslot;
   unsigned* cand_patch;
   unsigned patch_oct;
+  unsigned* n_out;               // != nullptr: *n_out = rowoff[n_index] (the list's length), by thread 0
+  long long n_index;
 };
 
 // Fills the deferred (NaN) candidate values of slots [0, *n) from the DoG planes.
@@ -278,6 +280,10 @@ hipError_t launch_seed0(const Pyramid& P, double* next, hipStream_t st);
 hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, int o_begin, int o_end);
 inline int extrema_words_per_row(int w) { return (w + kXW - 1) / kXW; }
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st);
+// Zeroes up to three word ranges in one launch (the extrema stage's counters
+// and row counts: one kernel instead of hipMemsetAsync's body + tail fills each).
+hipError_t launch_zero_words(unsigned* a, long long na, unsigned* b, long long nb, unsigned* c, long long nc,
+                             hipStream_t st);
 // One wave per ambiguous candidate: fp64 pointwise recompute of the 3x3x3 DoG patch.
 // Persistent grid over the device-side count of ambiguous keys (no host sync).
 hipError_t launch_exact_extrema(const Pyramid& P, const ExactLaunch& X, hipStream_t st);
