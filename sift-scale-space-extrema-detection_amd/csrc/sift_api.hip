@@ -183,9 +183,6 @@ struct sift_ctx {
   hipEvent_t ev[8]{};
   hipEvent_t ev_heavy = nullptr;  // after the last bandwidth-heavy kernel of a detection (sift_order_after)
   hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
-  // Concurrent octaves (octave_streams): octaves >= 1 on a side stream beside octave 0
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   sift_timings tm{};
   std::vector<double> oct_ms;      // per-octave Gaussian+DoG launch time of the last build
 };
@@ -353,9 +350,6 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   ctx->hpl.release();
   for (auto& e : ctx->ev_pl)
     if (e) (void)hipEventDestroy(e);
-  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
   if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -620,26 +614,9 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     ctx->xseed_w = (P.oct[P.O - 1].w + 1) / 2;
     HIPCHK(ctx->xseed.ensure((size_t)ctx->xseed_h * ctx->xseed_w * sizeof(double)));
   }
-  // Octaves >= 1 beside octave 0 (SIFT_OCONC, experiments): the octave-1 base
-  // comes straight from the input (launch_seed0, bit-identical to the
-  // octave-0 launch's seeds), so octaves 1.. run on a side stream while
-  // octave 0 runs on the context's; the pass ends when both have.
-  static const int oconc = exp_knob("SIFT_OCONC", 0);
-  const bool conc = oconc && o_first == 0 && so_end <= o_first && nimg == 1 && !nf && P.O >= 2 &&
-                    !gauss_needs_base0(P) && P.oct[0].rad[P.S] <= 16;
-  if (conc) {
-    if (!ctx->side) {
-      HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-    }
-    HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
-    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-    HIPCHK(launch_seed0(P, ctx->seeds.as<double>() + P.oct[1].seed_off, ctx->side));
-  }
   for (int o = o_first; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
-    hipStream_t ost = conc && o >= 1 ? ctx->side : ctx->stream;
+    hipStream_t ost = ctx->stream;
     if (o < so_end) {
       HIPCHK(launch_seed_only(P, o, ctx->seeds.as<double>() + oc.seed_off, ctx->seedv.as<double>(),
                               ctx->seeds.as<double>() + P.oct[o + 1].seed_off, ctx->stream));
@@ -676,14 +653,9 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.base_bs = o == 0 ? 0 : seeds_pi;
     L.l64_bs = P.l64_bstride;
     L.vsplit_bs = ctx->vsplit_pi;
-    if (conc && o == 0) L.next_seed = nullptr;  // launch_seed0 made it
     HIPCHK(launch_gauss_dog(P, L, ost));
     if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ost));
     HIPCHK(hipEventRecord(ctx->ev_go[o], ost));
-  }
-  if (conc) {
-    HIPCHK(hipEventRecord(ctx->ev_join, ctx->side));
-    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
   }
   HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
   ctx->dog_source = kNative;
@@ -1188,53 +1160,7 @@ static int refine_enqueue(sift_ctx* ctx) {
       R.patch = ctx->patch.as<float>();
     }
     static const int band_order = exp_knob("SIFT_BAND_ORDER", 1);
-    // strip order (SIFT_REFINE_STRIP = bitmap words per strip, 0 = whole
-    // rows: band order): pieces (octave, band, strip, scale, row)
-    static const int strip_words = exp_knob("SIFT_REFINE_STRIP", 0);
-    if (band_order && ctx->slots_rows && strip_words > 0) {
-      BandOrder B{};
-      B.n_oct = P.O;
-      B.S = P.S;
-      B.strip_words = strip_words;
-      int pieces = 0;
-      for (int o = 0; o < P.O; ++o) {
-        B.piece_off[o] = pieces;
-        B.row_off[o] = (int)ctx->x_row_off[o];
-        B.nw[o] = ctx->x_nw[o];
-        B.word_off[o] = ctx->x_word_off[o];
-        B.nstrip[o] = (ctx->x_nw[o] + strip_words - 1) / strip_words;
-        pieces += ((P.oct[o].h + kBandRows - 1) / kBandRows) * B.nstrip[o] * P.S * kBandRows;
-      }
-      B.piece_off[P.O] = pieces;
-      B.row_off[P.O] = ctx->xl.rows_per_img;
-      B.rows_per_img = ctx->xl.rows_per_img;
-      B.words_per_img = ctx->xl.words_per_img;
-      B.n_rows = ctx->xl.rows_per_img * std::max(1, P.nimg);
-      pieces *= std::max(1, P.nimg);
-      B.n_items = pieces;
-      HIPCHK(ctx->band_cnt.ensure((size_t)pieces * sizeof(unsigned)));
-      HIPCHK(ctx->band_first.ensure((size_t)pieces * sizeof(unsigned)));
-      HIPCHK(ctx->band_start.ensure((size_t)pieces * sizeof(unsigned)));
-      HIPCHK(ctx->perm.ensure((size_t)cap * sizeof(unsigned)));
-      B.bitmap = ctx->bitmap.as<unsigned long long>();
-      B.rowoff = ctx->rowoff.as<unsigned>();
-      B.count = ctx->band_cnt.as<unsigned>();
-      B.first = ctx->band_first.as<unsigned>();
-      B.start = ctx->band_start.as<unsigned>();
-      B.perm = ctx->perm.as<unsigned>();
-      B.cap = cap;
-      HIPCHK(hipMemsetAsync(B.count, 0, (size_t)pieces * sizeof(unsigned), ctx->stream));
-      HIPCHK(launch_strip_pieces(P, B, ctx->stream));
-      size_t tb = 0;
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, B.count, ctx->band_start.as<unsigned>(), pieces,
-                                              ctx->stream));
-      HIPCHK(ctx->temp.ensure(tb));
-      tb = ctx->temp.bytes;
-      HIPCHK(hipcub::DeviceScan::ExclusiveSum(ctx->temp.p, tb, B.count, ctx->band_start.as<unsigned>(), pieces,
-                                              ctx->stream));
-      HIPCHK(launch_piece_fill(B, ctx->stream));
-      R.perm = B.perm;
-    } else if (band_order && ctx->slots_rows) {
+    if (band_order && ctx->slots_rows) {
       BandOrder B{};
       B.n_oct = P.O;
       B.S = P.S;

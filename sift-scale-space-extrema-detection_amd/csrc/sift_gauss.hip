@@ -1709,61 +1709,6 @@ __global__ __launch_bounds__(256) void k_seed_horz(const Pyramid P, int o, const
   next[(long long)yp * nw + xp] = acc;
 }
 
-// The base of octave 1 straight from the input (the octave-0 launch need not
-// run first): seed[i][j] = L0[S][2i][2j] with octave 0's fma chains --
-// vertical sums of the 2x upsample B[y][x] = I[y >> 1][x >> 1] (clamped),
-// taps in increasing order from 0.0, then horizontal sums -- so the values
-// are bit-identical to the ones the octave-0 kernel writes (the vertical sums
-// depend on x only through x >> 1: one per input column).  A block owns 64
-// seed columns x 8 seed rows: the vertical sums of its 8 rows (upsampled rows
-// 2i) over the input columns the horizontal taps reach go to LDS, then one
-// lane per seed column runs the horizontal sums of the 8 rows.
-constexpr int kS0X = 64, kS0Y = 8;
-__global__ __launch_bounds__(256) void k_seed0(const Pyramid P, double* __restrict__ next, int next_w) {
-  __shared__ double vs[kS0Y][kS0X + 2 * 9 + 2];  // input columns j0 - hr .. j0 + 63 + hr (hr = ceil(r/2) <= 8)
-  const Octave& oc = P.oct[0];
-  const int r = oc.rad[P.S];
-  const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[P.S]);
-  const int h0 = oc.h, w0 = oc.w;  // 2H x 2W
-  const int h1 = P.oct[1].h;
-  const int j0 = blockIdx.x * kS0X, i0 = blockIdx.y * kS0Y;
-  const int hr = (r + 1) >> 1;
-  const int ncol = kS0X + 2 * hr;  // input columns j0 - hr .. j0 + 63 + hr
-  // vertical: item = (seed row t, input column c); B row y - r + k, y = 2 (i0 + t)
-  for (int it = threadIdx.x; it < kS0Y * ncol; it += 256) {
-    const int t = it / ncol, c = it - t * ncol;
-    const int y = 2 * (i0 + t);
-    const int xc = clampi(j0 - hr + c, 0, P.W - 1);  // input column (the upsampled column's x >> 1, clamped)
-    const float* col = P.img + xc;
-    double acc = 0.0;
-    for (int k = 0; k <= 2 * r; ++k)
-      acc = fma((double)wp[k], (double)col[(long long)(clampi(y - r + k, 0, h0 - 1) >> 1) * P.img_stride], acc);
-    vs[t][c] = acc;
-  }
-  __syncthreads();
-  // horizontal: seed (i0 + t, j0 + q), upsampled x = 2 (j0 + q); tap k reads
-  // upsampled column clamp(x - r + k), i.e. input column clamp(..) >> 1
-  const int q = threadIdx.x & 63;
-  const int j = j0 + q, x = 2 * j;
-  for (int t = threadIdx.x >> 6; t < kS0Y; t += 4) {
-    const int i = i0 + t;
-    if (i >= h1 || j >= next_w) continue;
-    double acc = 0.0;
-    for (int k = 0; k <= 2 * r; ++k) {
-      const int xi = clampi(x - r + k, 0, w0 - 1) >> 1;  // input column
-      acc = fma((double)wp[k], vs[t][xi - (j0 - hr)], acc);
-    }
-    next[(long long)i * next_w + j] = acc;
-  }
-}
-
-hipError_t launch_seed0(const Pyramid& P, double* next, hipStream_t st) {
-  if (P.O < 2 || !next || gauss_needs_base0(P) || P.oct[0].rad[P.S] > 16) return hipErrorInvalidValue;
-  const int w1 = P.oct[1].w, h1 = P.oct[1].h;
-  hipLaunchKernelGGL(k_seed0, dim3((w1 + kS0X - 1) / kS0X, (h1 + kS0Y - 1) / kS0Y), dim3(256), 0, st, P, next, w1);
-  return hipGetLastError();
-}
-
 size_t seed_only_scratch(const Pyramid& P, int o) {
   return (size_t)P.oct[o + 1].h * P.oct[o].w;
 }

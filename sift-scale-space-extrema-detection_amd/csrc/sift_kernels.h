@@ -225,20 +225,7 @@ struct BandOrder {
   unsigned* perm;                 // out: position -> slot
   int cap;
   int rows_per_img;               // batch: rowoff rows per image (items are image-major, item_off per image)
-  // Strip order (strip_words > 0): pieces (octave, band, strip of strip_words
-  // bitmap words, scale, band row) instead of items (octave, band, scale), so
-  // the candidates whose patches share DoG lines are a few slots apart.
-  int strip_words;
-  int piece_off[kMaxOctaves + 1];  // first piece of each octave (per image)
-  int nstrip[kMaxOctaves];         // strips per row
-  int nw[kMaxOctaves];             // bitmap words per row
-  long long word_off[kMaxOctaves]; // first bitmap word of each octave
-  long long words_per_img;
-  const unsigned long long* bitmap;
-  int n_rows;                      // rows (o, s, y) of all images: one wave each in k_strip_pieces
 };
-hipError_t launch_strip_pieces(const Pyramid& P, const BandOrder& B, hipStream_t st);
-hipError_t launch_piece_fill(const BandOrder& B, hipStream_t st);
 hipError_t launch_band_items(const Pyramid& P, const BandOrder& B, hipStream_t st);
 hipError_t launch_band_fill(const Pyramid& P, const BandOrder& B, hipStream_t st);
 
@@ -273,7 +260,6 @@ bool gauss_vsplit(const Pyramid& P, int o);
 // Octave o (>= 1) runs k_gauss_rw (register-window tiles, 224 columns x 8 rows; no split pass).
 bool gauss_wide(const Pyramid& P, int o);
 // The octave-1 base straight from the input (bit-identical to the octave-0 launch's seeds).
-hipError_t launch_seed0(const Pyramid& P, double* next, hipStream_t st);
 
 // Fills the unit table of L (octave geometry) and launches the scan; returns
 // the launch error.  L.bitmap words per octave: S * h * nw.

@@ -635,77 +635,6 @@ __global__ __launch_bounds__(256) void k_band_fill(const Pyramid P, const BandOr
     if (st + j < (unsigned)B.cap) B.perm[st + j] = f + j;
 }
 
-// Strip order pieces: one wave per row (image, octave, scale, y) of the
-// extrema stage.  Its bitmap words give each strip's candidate count and the
-// slot of its first candidate (row offset + the candidates of the strips
-// before it); the piece (octave, band, strip, scale, y - band start) of the
-// new order receives them.  Pieces of rows past the plane stay zero.
-__global__ __launch_bounds__(256) void k_strip_pieces(const Pyramid P, const BandOrder B) {
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row (image-major)
-  const int lane = threadIdx.x & 63;
-  if (g >= B.n_rows) return;
-  const int rpi = B.rows_per_img;
-  const int im = g / rpi, gl = g - im * rpi;
-  int o = 0;
-  while (o + 1 < B.n_oct && gl >= B.row_off[o + 1]) ++o;
-  const int h = P.oct[o].h, nw = B.nw[o], SW = B.strip_words;
-  const int row = gl - B.row_off[o], s = row / h + 1, y = row - (s - 1) * h;
-  if (y < 1 || y > h - 2) return;  // border rows: no candidates, their bitmap words are never written
-  const int band = y / kBandRows, yb = y - band * kBandRows;
-  const unsigned long long* bm = B.bitmap + im * B.words_per_img + B.word_off[o] + (long long)row * nw;
-  const unsigned r0 = B.rowoff[g];
-  const int ppi = B.piece_off[B.n_oct];
-  // piece (band, strip, s, yb) of octave o
-  const long long pbase = (long long)im * ppi + B.piece_off[o] +
-                          ((long long)band * B.nstrip[o]) * (B.S * kBandRows) + (s - 1) * kBandRows + yb;
-  unsigned before = 0;  // candidates of the row's earlier word chunks
-  for (int w0 = 0; w0 < nw; w0 += 64) {
-    const int w = w0 + lane;
-    const unsigned c = w < nw ? (unsigned)__popcll(bm[w]) : 0u;
-    unsigned inc = c;  // inclusive wave scan
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned t = __shfl_up(inc, off);
-      if (lane >= off) inc += t;
-    }
-    // the lane holding a strip's first word writes the strip's piece: its
-    // count = inclusive sum at the strip's last word - exclusive sum at its
-    // first (64 % SW == 0: a chunk of 64 words holds whole strips)
-    const bool head = w < nw && w % SW == 0;
-    const int last = head ? min(nw - 1, w + SW - 1) - w0 : lane;
-    const unsigned end_inc = __shfl(inc, last);  // all lanes take part
-    if (head) {
-      const long long pc = pbase + (long long)(w / SW) * (B.S * kBandRows);
-      B.first[pc] = r0 + before + inc - c;
-      B.count[pc] = end_inc - (inc - c);
-    }
-    before += __shfl(inc, 63);
-  }
-}
-
-// One thread per piece (most hold 0-2 candidates): its slots in order at its
-// position of the new order.
-__global__ __launch_bounds__(256) void k_piece_fill(const BandOrder B) {
-  const int it = blockIdx.x * 256 + threadIdx.x;
-  if (it >= B.n_items) return;
-  const unsigned c = B.count[it], f = B.first[it], st = B.start[it];
-  for (unsigned j = 0; j < c; ++j)
-    if (st + j < (unsigned)B.cap) B.perm[st + j] = f + j;
-}
-
-hipError_t launch_strip_pieces(const Pyramid& P, const BandOrder& B, hipStream_t st) {
-  if (B.n_rows <= 0) return hipSuccess;
-  if (B.strip_words < 1 || 64 % B.strip_words) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_strip_pieces, dim3((B.n_rows + 3) / 4), dim3(256), 0, st, P, B);
-  return hipGetLastError();
-}
-
-hipError_t launch_piece_fill(const BandOrder& B, hipStream_t st) {
-  if (B.n_items <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_piece_fill, dim3((B.n_items + 255) / 256), dim3(256), 0, st, B);
-  return hipGetLastError();
-}
-
 hipError_t launch_band_items(const Pyramid& P, const BandOrder& B, hipStream_t st) {
   if (B.n_items <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_band_items, dim3((B.n_items + 255) / 256), dim3(256), 0, st, P, B);
