@@ -1760,7 +1760,11 @@ int sift_merge_keypoint_blocks_device(sift_ctx* ctx, const sift_keypoint* d_in, 
   tab.insert(tab.end(), cstart.begin(), cstart.end());
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(ctx->merge_tab.ensure(tab.size() * sizeof(long long)));
-  HIPCHK(hipMemcpyAsync(ctx->merge_tab.p, tab.data(), tab.size() * sizeof(long long), hipMemcpyHostToDevice,
+  // through the context's pinned staging (an asynchronous DMA; a pageable
+  // source is copied through the runtime's own staging first)
+  HIPCHK(ctx->hpl.ensure(tab.size() * sizeof(long long)));
+  std::memcpy(ctx->hpl.p, tab.data(), tab.size() * sizeof(long long));
+  HIPCHK(hipMemcpyAsync(ctx->merge_tab.p, ctx->hpl.p, tab.size() * sizeof(long long), hipMemcpyHostToDevice,
                         ctx->stream));
   HIPCHK(launch_merge_blocks(reinterpret_cast<const Keypoint*>(d_in), ctx->merge_tab.as<long long>(),
                              ctx->merge_tab.as<long long>() + 3 * (size_t)nseg, nseg, chunks,
