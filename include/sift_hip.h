@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 7
+#define SIFT_ABI_VERSION 8
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -197,6 +197,14 @@ int sift_copy_keypoints(struct sift_ctx *ctx, sift_keypoint *out, size_t cap, si
  * = abs_sigma, abs_x, abs_y, interp_value of keypoint i, in the reference's
  * order (background.js:660-671).  Through the context's pinned staging. */
 int sift_copy_keypoints_soa(struct sift_ctx *ctx, int32_t *ints, double *reals, size_t cap, size_t *n_out);
+
+/* Page-lock a caller's host buffer for the device's DMA engines (ABI version
+ * >= 8): plane and keypoint reads into a registered buffer are one
+ * device -> host DMA instead of a staged copy through pinned memory.  For
+ * buffers the caller recycles (the JS addon's result pool); unregister
+ * before freeing.  Registration faults in and pins every page. */
+int sift_host_register(void *p, size_t bytes);
+int sift_host_unregister(void *p);
 
 /* Override the two scalars refineCandidateKeypoints receives in its own
  * message (minBlurLevel, minInterpixelDistance: background.js:460-461,

@@ -213,9 +213,20 @@ static int check_params(const sift_params* p) {
 // between the two halves of ctx->hpl, so the DMA of chunk i+1 overlaps the
 // (multi-threaded) host copy of chunk i.  A plain hipMemcpy into pageable
 // memory runs at a fraction of the link rate; this keeps the link busy.
+// Host memory the runtime can DMA into directly (sift_host_register /
+// hipHostMalloc); anything else is pageable.
+static bool host_registered(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is an error here, not a failure
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 static hipError_t d2h_staged(sift_ctx* ctx, void* dst, const void* src, size_t bytes) {
   constexpr size_t kChunk = (size_t)8 << 20;
-  if (bytes < ((size_t)1 << 20)) {  // small: one DMA straight into the destination
+  if (bytes < ((size_t)1 << 20) || host_registered(dst)) {  // small or page-locked: one DMA straight into it
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
     return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
   }
@@ -247,6 +258,16 @@ static hipError_t d2h_staged(sift_ctx* ctx, void* dst, const void* src, size_t b
 extern "C" {
 
 int sift_abi_version(void) { return SIFT_ABI_VERSION; }
+
+int sift_host_register(void* p, size_t bytes) {
+  if (!p || !bytes) return SIFT_E_ARG;
+  return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? SIFT_OK : SIFT_E_HIP;
+}
+
+int sift_host_unregister(void* p) {
+  if (!p) return SIFT_E_ARG;
+  return hipHostUnregister(p) == hipSuccess ? SIFT_OK : SIFT_E_HIP;
+}
 
 int sift_params_default(sift_params* p) {
   if (!p) return SIFT_E_ARG;

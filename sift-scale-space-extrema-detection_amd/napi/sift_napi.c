@@ -163,19 +163,26 @@ static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
 /* Large buffers are anonymous mappings advised as transparent huge pages:
  * a fresh buffer then faults once per 2 MiB instead of once per 4 KiB
  * (first-touch memset 11 -> 18 GB/s, profiles/r4p_d2h_probe.txt). */
+/* ... and page-locked for the device (sift_host_register): a recycled
+ * buffer then takes plane and keypoint reads as one DMA (no staged copy). */
 static void *big_alloc(size_t bytes) {
   void *p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (p == MAP_FAILED) return NULL;
 #ifdef MADV_HUGEPAGE
   madvise(p, bytes, MADV_HUGEPAGE);
 #endif
+  (void)sift_host_register(p, bytes); /* on failure the reads are staged */
   return p;
 }
 
 static void big_free(void *p, size_t bytes) {
   if (!p) return;
-  if (bytes >= POOL_MIN_BYTES) munmap(p, bytes);
-  else free(p);
+  if (bytes >= POOL_MIN_BYTES) {
+    (void)sift_host_unregister(p);
+    munmap(p, bytes);
+  } else {
+    free(p);
+  }
 }
 
 static void *pool_take(size_t bytes) {

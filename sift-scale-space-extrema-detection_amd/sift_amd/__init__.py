@@ -46,7 +46,7 @@ ABI_SYMBOLS = (
     "sift_last_error", "sift_schedule", "sift_octave_dims", "sift_build_scale_space",
     "sift_build_scale_space_device", "sift_get_dims", "sift_get_blur_level", "sift_get_plane",
     "sift_load_dog", "sift_load_scale_space", "sift_find_extrema", "sift_refine",
-    "sift_set_candidates", "sift_refine_params", "sift_copy_candidates", "sift_copy_keypoints", "sift_copy_keypoints_soa",
+    "sift_set_candidates", "sift_refine_params", "sift_copy_candidates", "sift_copy_keypoints", "sift_copy_keypoints_soa", "sift_host_register", "sift_host_unregister",
     "sift_copy_keypoints_device", "sift_detect", "sift_detect_device", "sift_last_counts",
     "sift_last_timings", "sift_device_keypoints", "sift_stream", "sift_synchronize",
     "sift_detect_device_async", "sift_detect_wait", "sift_ctx_create_shared",
@@ -147,6 +147,8 @@ def lib():
         "sift_set_flags": (ctypes.c_int, [vp, ctypes.c_int]),
         "sift_copy_keypoints": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_copy_keypoints_soa": (ctypes.c_int, [vp, vp, vp, sz, szp]),
+        "sift_host_register": (ctypes.c_int, [vp, sz]),
+        "sift_host_unregister": (ctypes.c_int, [vp]),
         "sift_copy_keypoints_device": (ctypes.c_int, [vp, vp, sz, szp]),
         "sift_detect": (ctypes.c_int, [vp, fp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
         "sift_detect_device": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, sz, pp, vp, sz, szp]),
