@@ -163,22 +163,37 @@ static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
 /* Large buffers are anonymous mappings advised as transparent huge pages:
  * a fresh buffer then faults once per 2 MiB instead of once per 4 KiB
  * (first-touch memset 11 -> 18 GB/s, profiles/r4p_d2h_probe.txt). */
-/* ... and page-locked for the device (sift_host_register): a recycled
- * buffer then takes plane and keypoint reads as one DMA (no staged copy). */
 static void *big_alloc(size_t bytes) {
   void *p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (p == MAP_FAILED) return NULL;
 #ifdef MADV_HUGEPAGE
   madvise(p, bytes, MADV_HUGEPAGE);
 #endif
-  (void)sift_host_register(p, bytes); /* on failure the reads are staged */
   return p;
+}
+
+/* Recycled buffers are page-locked for the device (sift_host_register, on
+ * their first reuse: registering a fresh buffer costs what its first touch
+ * does, so one-shot results stay unregistered): plane and keypoint reads
+ * into them are one DMA (56 GB/s against 33 GB/s staged,
+ * profiles/r4ak_plane_readback_probe.json).  g_reg lists them (pool lock). */
+static void *g_reg[2 * POOL_SLOTS];
+static int g_reg_n = 0;
+
+static int reg_find(void *p) {
+  for (int i = 0; i < g_reg_n; ++i)
+    if (g_reg[i] == p) return i;
+  return -1;
 }
 
 static void big_free(void *p, size_t bytes) {
   if (!p) return;
   if (bytes >= POOL_MIN_BYTES) {
-    (void)sift_host_unregister(p);
+    pthread_mutex_lock(&g_pool_mu);
+    const int i = reg_find(p);
+    if (i >= 0) g_reg[i] = g_reg[--g_reg_n];
+    pthread_mutex_unlock(&g_pool_mu);
+    if (i >= 0) (void)sift_host_unregister(p);
     munmap(p, bytes);
   } else {
     free(p);
@@ -193,6 +208,8 @@ static void *pool_take(size_t bytes) {
         void *p = g_pool[i].p;
         g_pool[i] = g_pool[--g_pool_n];
         g_pool_bytes -= bytes;
+        const int reg = reg_find(p) >= 0 || g_reg_n >= 2 * POOL_SLOTS;
+        if (!reg && sift_host_register(p, bytes) == SIFT_OK) g_reg[g_reg_n++] = p;  /* first reuse */
         pthread_mutex_unlock(&g_pool_mu);
         return p;
       }
