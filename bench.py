@@ -183,9 +183,10 @@ def main():
                     help="with --batch B > 1: launch = the B images as ONE batched detection per step "
                          "(sift_detect_batch_device: one launch per stage over the batch), images = B separate "
                          "detections per step")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="detections in flight per GPU (one context each; the host settles image k while "
-                         "image k+1 runs)")
+                         "image k+1 runs).  Default: 2 for single images (4K: 2 > 3 by 1.5-2 %%, "
+                         "profiles/r4am_inflight_ab.txt), 3 for batched launches (cfg 4: 3 > 2 by 3 %%, DESIGN 8a)")
     ap.add_argument("--overlap", default="octave0",
                     choices=["none", "octave0", "gaussian", "refinement", "full", "phased"],
                     help="how consecutive images overlap on the GPU: none = contexts share one stream; "
@@ -249,7 +250,7 @@ def main():
         d_imgs = torch.from_numpy(np.stack([img] + [blob_image(W, H, seed=1000 + 64 * rank + i)
                                                    for i in range(1, Bt)])).to("cuda:%d" % dev)
     torch.cuda.synchronize(dev)
-    nin = max(1, args.inflight)
+    nin = max(1, args.inflight if args.inflight is not None else (3 if args.batch > 1 else 2))
     ctxs = [sift_amd.Context(dev)]
     own = args.overlap != "none"
     after = {"octave0": sift_amd.AFTER_OCTAVE0, "gaussian": sift_amd.AFTER_GAUSSIAN,
