@@ -16,9 +16,10 @@ pass (one k_gauss_dog launch per octave): B_alg = 4WH + sum_o 4 P_o (S+3) +
 sum_o 4 P_o (S+2) (the input read, every Gaussian and DoG plane written in
 fp32) divided by the pass's HIP-event time on the context's stream, one image
 at a time; `per_octave`, `pipelined`, `octave0` and `extrema_stage` break it
-down.  `traffic` is the pass's HBM bytes from the committed rocprofv3 PMC
-summary (profiles/*pmc*.json, tools/pmc_launches.py) when it matches the
-config.  `sustained` re-runs the pipelined loop for --sustain-s seconds after
+down.  `traffic` is the pass's HBM bytes (every pass launch of one image)
+from the rocprofv3 PMC summary of the latest round (profiles/*pmc*.json,
+tools/pmc_launches.py, or --pmc) when it matches the config, split per
+octave in `per_octave[o].traffic`.  `sustained` re-runs the pipelined loop for --sustain-s seconds after
 the timed region (a steady-state rate over thousands of images, beside the
 K-step `value`).
 """
@@ -27,6 +28,7 @@ import glob
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -86,18 +88,29 @@ def extrema_bytes(W, H, O, S):
     return sum(4 * h * w * (S + 2) for h, w in octave_dims(W, H, O))
 
 
-def load_traffic(cfg_key, field="hbm_bytes_per_launch"):
-    """HBM bytes per launch (or per pass: field="pass_hbm_bytes") from the
-    newest committed PMC summary for this configuration (profiles/*pmc*.json,
-    tools/pmc_launches.py / tools/pmc_traffic.py)."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+def _round_key(path):
+    """Sort key of a profile's round tag: r4v < r4al < r5a (round, then the
+    letter suffix in a..z, aa..az order)."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    if not m:
+        return (-1, 0, "")
+    return (int(m.group(1)), len(m.group(2)), m.group(2))
+
+
+def load_pmc(cfg_key, path=None):
+    """The PMC summary of this configuration (tools/pmc_launches.py): the one
+    named by --pmc, else the committed profiles/*pmc*.json of the latest
+    round tag whose config_key matches."""
+    paths = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")),
+                                       key=_round_key, reverse=True)
+    for p in paths:
         try:
-            with open(path) as f:
+            with open(p) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("config_key") == cfg_key and d.get(field):
-            return float(d[field]), os.path.relpath(path, ROOT)
+        if d.get("config_key") == cfg_key and d.get("pass_hbm_bytes"):
+            return d, os.path.relpath(p, ROOT)
     return None, None
 
 
@@ -202,6 +215,9 @@ def main():
                     help="seconds of the same pipelined loop after the timed region, reported as `sustained` "
                          "(0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=None,
+                    help="PMC summary (tools/pmc_launches.py) for roofline.traffic; default: the committed "
+                         "profiles/*pmc*.json of the latest round tag for this configuration")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop WxH timed on the CPU oracle")
     ap.add_argument("--cpu-sample-js", default="1920x1080",
                     help="crop WxH timed on the single-threaded JS restatement (the C port's crop; about 15 s on the GPU box)")
@@ -424,8 +440,12 @@ def main():
         B0 = Bo[0]
         gbs = lambda b, ms: b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         cfg_key = "%dx%d_o%d_s%d%s" % (W, H, O, S, "_nogauss" if args.skip_gauss_planes else "")
-        pass_traffic, pass_src = load_traffic(cfg_key, "pass_hbm_bytes")
-        oct0_traffic, oct0_src = load_traffic(cfg_key)
+        pmc, pmc_src = load_pmc(cfg_key, args.pmc)
+        pass_traffic = pmc["pass_hbm_bytes"] if pmc else None
+        oct0_traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        oct_traffic = {}
+        for r in (pmc or {}).get("per_octave", []):
+            oct_traffic[tuple(r["octaves"])] = r["hbm_bytes"]
         pipelined_note = ("pipelined: %d images in flight on %d streams, each launch's window includes "
                           "waiting for CUs held by the other images' kernels" % (nin, nin)
                           if own and nin > 1 else "one image at a time")
@@ -480,7 +500,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(gbs(B, iso_pass) / HBM_PEAK_GBS, 4),
                 "traffic": pass_traffic,
-                "traffic_source": pass_src,
+                "traffic_source": pmc_src,
                 "alg_bytes_per_launch": B,
                 "alg_bytes_formula": ("4WH + sum_o 4P_o(S+2) + sum_{o>=1} 8P_o" if args.skip_gauss_planes
                                       else "4WH + sum_o 4P_o(S+3) + sum_o 4P_o(S+2)"),
@@ -492,7 +512,9 @@ def main():
                 "per_octave": [
                     {"octave": o, "plane": list(octave_dims(W, H, O)[o]), "alg_bytes": Bo[o],
                      "iso_ms": round(iso_oct[o], 5), "iso_frac": round(gbs(Bo[o], iso_oct[o]) / HBM_PEAK_GBS, 4),
-                     "pipelined_ms": round(oct_ms[o] / NI, 5)}
+                     "pipelined_ms": round(oct_ms[o] / NI, 5),
+                     "traffic": next((v for k, v in oct_traffic.items() if o in k), None),
+                     "traffic_octaves": next((list(k) for k in oct_traffic if o in k), None)}
                     for o in range(O)],
                 "pipelined": {
                     "what": "the same pass inside the timed region (%s), HIP events, averaged over %d images" %
@@ -509,7 +531,7 @@ def main():
                     "pipelined_ms": round(oct0_ms, 5),
                     "pipelined_frac": round(gbs(B0, oct0_ms) / HBM_PEAK_GBS, 4),
                     "traffic": oct0_traffic,
-                    "traffic_source": oct0_src,
+                    "traffic_source": pmc_src,
                 },
                 "extrema_stage": {
                     "what": "extrema stage (scan of every DoG plane + ordered emission + exact re-decisions), "

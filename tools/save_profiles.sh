@@ -6,7 +6,7 @@ T=$1
 R=$(cd "$(dirname "$0")/.." && pwd)
 G=$R/gpurun_out
 P=$R/profiles
-python3 $R/tools/pmc_launches.py --config-key 3840x2160_o4_s5 --out $P/${T}_pmc_4k_o4_s5.json $G/pmc_${T}_FETCH_SIZE $G/pmc_${T}_WRITE_SIZE $G/pmc_${T}_TA $( [ -d $G/pmc_${T}_SQ ] && echo $G/pmc_${T}_SQ ) > $P/${T}_pmc_4k_o4_s5.txt
+python3 $R/tools/pmc_launches.py --config-key 3840x2160_o4_s5 --round $T --out $P/${T}_pmc_4k_o4_s5.json $G/pmc_${T}_FETCH_SIZE $G/pmc_${T}_WRITE_SIZE $G/pmc_${T}_TA $( [ -d $G/pmc_${T}_SQ ] && echo $G/pmc_${T}_SQ ) > $P/${T}_pmc_4k_o4_s5.txt
 cp $G/prof_${T}/run_kernel_stats.csv $P/${T}_4k_o4_s5_kernel_stats.csv
 cp $G/prof_${T}_iso/run_kernel_stats.csv $P/${T}_iso_4k_o4_s5_kernel_stats.csv
 python3 $R/tools/kstats.py $P/${T}_4k_o4_s5_kernel_stats.csv > $P/${T}_4k_o4_s5_kernel_stats.txt
