@@ -372,6 +372,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
   for (auto& e : ctx->ev_pl)
     if (e) (void)hipEventDestroy(e);
   if (ctx->h_counters) (void)hipHostFree(ctx->h_counters);
+  ctx->seedv.release();
   if (ctx->stream && ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return SIFT_OK;

@@ -95,6 +95,7 @@ constexpr bool kVert2 = SIFT_VERT2 != 0;
 #endif
 constexpr bool kVertGen2 = SIFT_VGEN2 != 0;
 constexpr int kUR1 = SIFT_UR1;       // ... octaves >= 1 (SGPR budget: taps are SGPR operands)
+constexpr int kUR96 = kUR1 < 12 ? kUR1 : 12;  // ... 96-column tiles (96 + 2r columns in 64 lanes x 2)
 constexpr int kCG = kGX / 4;         // column groups of 4 outputs (16)
 constexpr int kRS = 64 / kCG;        // row sub-groups per wave (4)
 constexpr int kNR = 8 / kRS;         // rows per lane in the horizontal pass (2)
@@ -1560,7 +1561,7 @@ static bool staged0(const Pyramid& P, int o) { return o == 0 && !gauss_needs_bas
 static int tile_w(const Pyramid& P, int o) {
   static const int tw96 = exp_knob("SIFT_TW96", 1);
   const Octave& oc = P.oct[o];
-  return (tw96 && o >= 1 && kVert2 && oc.rmax <= kUR1 && oc.w >= 2 && !gauss_vsplit(P, o)) ? 96 : kGX;
+  return (tw96 && o >= 1 && kVert2 && oc.rmax <= kUR96 && oc.w >= 2 && !gauss_vsplit(P, o)) ? 96 : kGX;
 }
 
 constexpr int kSW0 = 2 * (kCG - 1) + 8 + 6;   // octave-0 strip stride for rmax <= 8
@@ -1825,7 +1826,7 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     set_attr<true, kSW0, 8, false>();
     set_attr<true, kSW1, kUR, false>();
     set_attr<false, 0, kUR1, false>();
-    (void)hipFuncSetAttribute((const void*)k_gauss_dog<false, 0, kUR1, false, 96>,
+    (void)hipFuncSetAttribute((const void*)k_gauss_dog<false, 0, kUR96, false, 96>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     set_attr<true, kSW0, 8, true>();
     set_attr<true, kSW1, kUR, true>();
@@ -1848,7 +1849,7 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     if (L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, true>), grid, dim3(256), lds, st, P, L);
     else hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, true>), grid, dim3(256), lds, st, P, L);
   } else if (tw == 96) {
-    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false, 96>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
+    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR96, false, 96>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
   } else if (staged0(P, L.o) && L.sw == kSW0) {
     hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, false>), grid, dim3(256), lds, st, P, L);
   } else if (staged0(P, L.o)) {
