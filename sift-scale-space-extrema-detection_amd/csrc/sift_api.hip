@@ -9,6 +9,8 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -213,20 +215,26 @@ static int check_params(const sift_params* p) {
 // between the two halves of ctx->hpl, so the DMA of chunk i+1 overlaps the
 // (multi-threaded) host copy of chunk i.  A plain hipMemcpy into pageable
 // memory runs at a fraction of the link rate; this keeps the link busy.
-// Host memory the runtime can DMA into directly (sift_host_register /
-// hipHostMalloc); anything else is pageable.
-static bool host_registered(const void* p) {
-  hipPointerAttribute_t a{};
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();  // pageable memory is an error here, not a failure
-    return false;
-  }
-  return a.type == hipMemoryTypeHost;
+// Host ranges page-locked through sift_host_register: the runtime DMAs into
+// them directly; anything else is treated as pageable.  Tracked here rather
+// than probed with hipPointerGetAttributes, whose failure on pageable memory
+// would have to be cleared with hipGetLastError -- and that would also
+// swallow an earlier asynchronous error still pending on the thread.
+static std::mutex g_reg_mu;
+static std::map<uintptr_t, size_t> g_reg_ranges;  // start -> bytes
+
+static bool host_registered(const void* p, size_t bytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg_ranges.upper_bound(a);
+  if (it == g_reg_ranges.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->first + it->second;
 }
 
 static hipError_t d2h_staged(sift_ctx* ctx, void* dst, const void* src, size_t bytes) {
   constexpr size_t kChunk = (size_t)8 << 20;
-  if (bytes < ((size_t)1 << 20) || host_registered(dst)) {  // small or page-locked: one DMA straight into it
+  if (bytes < ((size_t)1 << 20) || host_registered(dst, bytes)) {  // small or page-locked: one DMA straight into it
     hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
     return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
   }
@@ -261,11 +269,18 @@ int sift_abi_version(void) { return SIFT_ABI_VERSION; }
 
 int sift_host_register(void* p, size_t bytes) {
   if (!p || !bytes) return SIFT_E_ARG;
-  return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? SIFT_OK : SIFT_E_HIP;
+  if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) return SIFT_E_HIP;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  g_reg_ranges[reinterpret_cast<uintptr_t>(p)] = bytes;
+  return SIFT_OK;
 }
 
 int sift_host_unregister(void* p) {
   if (!p) return SIFT_E_ARG;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg_ranges.erase(reinterpret_cast<uintptr_t>(p));
+  }
   return hipHostUnregister(p) == hipSuccess ? SIFT_OK : SIFT_E_HIP;
 }
 

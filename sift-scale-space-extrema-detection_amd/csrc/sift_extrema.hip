@@ -59,6 +59,15 @@ template <int NP>
 __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int row) {
   // buffer loads: lane byte offset in a VGPR, row + plane offset in an SGPR
   const unsigned rofs = (unsigned)row * (unsigned)U.w * 4u;
+#if defined(SIFT_X_PROBE2COL)  // timing probe: 8-byte loads, two columns per lane (half the waves)
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(
+        U.rsrc, (int)U.xoff, (int)(rofs + (unsigned)q * U.plane_bytes), SIFT_XLOAD_AUX);
+    dst[q] = __builtin_bit_cast(float, v[0]) + __builtin_bit_cast(float, v[1]);
+  }
+  return;
+#endif
 #pragma unroll
   for (int q = 0; q < NP; ++q)
     dst[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
@@ -206,6 +215,10 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   U.o = o;
   const int x = xw * kXW - 1 + U.lane;
   U.xoff = 4u * (unsigned)clampi(x, 0, oc.w - 1);
+#if defined(SIFT_X_PROBE2COL)
+  if (xw & 1) return;
+  U.xoff = 4u * (unsigned)clampi(2 * kXW * (xw >> 1) - 2 + 2 * U.lane, 0, oc.w - 2);
+#endif
   U.plane_bytes = (unsigned)(4 * U.plane);
   U.colmask = __ballot(U.lane >= 1 && U.lane <= kXW && x >= 1 && x <= oc.w - 2);
   U.base = P.dog + b * P.dog_bstride + oc.dog_off + (long long)(s_first - 1) * U.plane;

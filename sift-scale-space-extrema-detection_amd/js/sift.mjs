@@ -495,8 +495,11 @@ export function detectAsync(input_image, opts = {}) {
   return new Promise((resolve) => pool.waiters.push({ resolve, limit })).then(start);
 }
 
+// Counts and timings of the device's latest call: a synchronous one, or the
+// last detectAsync job to settle (whichever of the pool's contexts ran it).
 export function lastCounts(device = 0) {
-  return native.counts(deviceState(device).ctx);
+  const st = deviceState(device);
+  return native.counts(st.lastCtx || st.ctx);
 }
 
 // Device stage times of the last call chain on a device (HIP events, ms:
@@ -638,6 +641,13 @@ export function createWorkerHandler(post, { matrix2d = true, device = 0, preview
         console.log('sift worker received an unknown message:', m);
     }
   };
+}
+
+// The addon's recycled result buffers (>= 1 MiB planes and keypoint
+// fields): buffers and bytes held for reuse, buffers and bytes page-locked.
+export function poolStats() {
+  const [buffers, bytes, pinned, pinnedBytes] = native.poolStats();
+  return { buffers, bytes, pinned, pinnedBytes };
 }
 
 export const abiVersion = native.abiVersion();

@@ -144,21 +144,48 @@ static napi_value make_typed(napi_env env, napi_typedarray_type t, size_t n, siz
  * A fresh ArrayBuffer's pages fault on first touch: 10-19 GB/s into fresh
  * pages however many threads copy, against 56 GB/s of DMA into touched pages
  * (profiles/r4p_d2h_probe.txt).  Buffers of >= 1 MiB are external
- * ArrayBuffers that go back to this pool when V8 collects them (the sizes
- * recur: one geometry's planes and keypoint counts), so their pages stay
- * mapped; the external-memory accounting tells V8 to collect.  Finalizers run
- * on their environment's JS thread, detectAsync takes buffers on the libuv
- * pool: one lock. */
+ * ArrayBuffers that go back to this pool when V8 collects them, so their
+ * pages stay mapped; the external-memory accounting tells V8 to collect.
+ * Finalizers run on their environment's JS thread, detectAsync takes buffers
+ * on the libuv pool: one lock.
+ *
+ * Size classes: a request is served from a buffer of its class (2 MiB units,
+ * rounded up to 3 significant bits: at most 1/8 slack), so keypoint fields
+ * whose counts differ from image to image still reuse each other's buffers.
+ * A full pool evicts its least recently returned buffers (unmapped,
+ * unregistered) instead of refusing the new one, so the sizes in current
+ * use stay pooled whatever passed through before. */
 #define POOL_MIN_BYTES ((size_t)1 << 20)
-#define POOL_SLOTS 512
+#define POOL_SLOTS 256
 static struct {
   void *p;
-  size_t bytes;
+  size_t bytes; /* the class size (the mapping's length) */
+  unsigned long long stamp;
 } g_pool[POOL_SLOTS];
 static int g_pool_n = 0;
 static size_t g_pool_bytes = 0;
-static const size_t g_pool_cap = (size_t)8 << 30; /* bytes kept for reuse */
+static unsigned long long g_pool_clock = 0;
+static size_t g_pool_cap = (size_t)6 << 30;  /* bytes kept for reuse (SIFT_NAPI_POOL_MB) */
+static size_t g_reg_cap = (size_t)4 << 30;   /* bytes kept page-locked (SIFT_NAPI_PIN_MB) */
 static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_once_t g_pool_once = PTHREAD_ONCE_INIT;
+
+static void pool_caps(void) {
+  const char *e = getenv("SIFT_NAPI_POOL_MB");
+  if (e && *e) g_pool_cap = (size_t)strtoull(e, NULL, 10) << 20;
+  e = getenv("SIFT_NAPI_PIN_MB");
+  if (e && *e) g_reg_cap = (size_t)strtoull(e, NULL, 10) << 20;
+}
+
+/* The class of a request of >= POOL_MIN_BYTES bytes. */
+static size_t pool_class(size_t bytes) {
+  const size_t G = (size_t)2 << 20;
+  size_t n = (bytes + G - 1) / G;
+  int e = 0;
+  while ((n >> e) >= 16) ++e;
+  const size_t u = (size_t)1 << e;
+  return (n + u - 1) / u * u * G;
+}
 
 /* Large buffers are anonymous mappings advised as transparent huge pages:
  * a fresh buffer then faults once per 2 MiB instead of once per 4 KiB
@@ -174,24 +201,33 @@ static void *big_alloc(size_t bytes) {
 
 /* Recycled buffers are page-locked for the device (sift_host_register, on
  * their first reuse: registering a fresh buffer costs what its first touch
- * does, so one-shot results stay unregistered): plane and keypoint reads
- * into them are one DMA (56 GB/s against 33 GB/s staged,
- * profiles/r4ak_plane_readback_probe.json).  g_reg lists them (pool lock). */
-static void *g_reg[2 * POOL_SLOTS];
+ * does, so one-shot results stay unregistered), up to g_reg_cap bytes: plane
+ * and keypoint reads into them are one DMA (56 GB/s against 33 GB/s staged,
+ * profiles/r4ak_plane_readback_probe.json).  g_reg lists them (pool lock);
+ * the registration itself runs outside the lock. */
+static struct {
+  void *p;
+  size_t bytes;
+} g_reg[2 * POOL_SLOTS];
 static int g_reg_n = 0;
+static size_t g_reg_bytes = 0;
 
 static int reg_find(void *p) {
   for (int i = 0; i < g_reg_n; ++i)
-    if (g_reg[i] == p) return i;
+    if (g_reg[i].p == p) return i;
   return -1;
 }
 
+/* Unmap a class buffer (unregistering it first); small ones are malloc'ed. */
 static void big_free(void *p, size_t bytes) {
   if (!p) return;
   if (bytes >= POOL_MIN_BYTES) {
     pthread_mutex_lock(&g_pool_mu);
     const int i = reg_find(p);
-    if (i >= 0) g_reg[i] = g_reg[--g_reg_n];
+    if (i >= 0) {
+      g_reg_bytes -= g_reg[i].bytes;
+      g_reg[i] = g_reg[--g_reg_n];
+    }
     pthread_mutex_unlock(&g_pool_mu);
     if (i >= 0) (void)sift_host_unregister(p);
     munmap(p, bytes);
@@ -200,40 +236,102 @@ static void big_free(void *p, size_t bytes) {
   }
 }
 
+/* A buffer for a request of `bytes` (class size pool_class(bytes) when large). */
 static void *pool_take(size_t bytes) {
-  if (bytes >= POOL_MIN_BYTES) {
+  if (bytes < POOL_MIN_BYTES) {
+    void *p = NULL;
+    return posix_memalign(&p, 4096, bytes ? bytes : 1) ? NULL : p;
+  }
+  const size_t cls = pool_class(bytes);
+  void *p = NULL;
+  int do_reg = 0;
+  pthread_once(&g_pool_once, pool_caps);
+  pthread_mutex_lock(&g_pool_mu);
+  int best = -1;
+  for (int i = 0; i < g_pool_n; ++i)  /* the most recently returned buffer of the class */
+    if (g_pool[i].bytes == cls && (best < 0 || g_pool[i].stamp > g_pool[best].stamp)) best = i;
+  if (best >= 0) {
+    p = g_pool[best].p;
+    g_pool[best] = g_pool[--g_pool_n];
+    g_pool_bytes -= cls;
+    do_reg = reg_find(p) < 0 && g_reg_n < 2 * POOL_SLOTS && g_reg_bytes + cls <= g_reg_cap;
+    if (do_reg) {  /* reserve the record; filled in below */
+      g_reg[g_reg_n].p = NULL;
+      g_reg[g_reg_n].bytes = cls;
+      g_reg_n++;
+      g_reg_bytes += cls;
+    }
+  }
+  pthread_mutex_unlock(&g_pool_mu);
+  if (!p) return big_alloc(cls);
+  if (do_reg) {  /* first reuse: page-lock it, outside the lock */
+    const int ok = sift_host_register(p, cls) == SIFT_OK;
     pthread_mutex_lock(&g_pool_mu);
-    for (int i = g_pool_n - 1; i >= 0; --i)
-      if (g_pool[i].bytes == bytes) {
-        void *p = g_pool[i].p;
-        g_pool[i] = g_pool[--g_pool_n];
-        g_pool_bytes -= bytes;
-        const int reg = reg_find(p) >= 0 || g_reg_n >= 2 * POOL_SLOTS;
-        if (!reg && sift_host_register(p, bytes) == SIFT_OK) g_reg[g_reg_n++] = p;  /* first reuse */
-        pthread_mutex_unlock(&g_pool_mu);
-        return p;
+    for (int i = g_reg_n - 1; i >= 0; --i)
+      if (g_reg[i].p == NULL && g_reg[i].bytes == cls) {
+        if (ok) {
+          g_reg[i].p = p;
+        } else {
+          g_reg_bytes -= cls;
+          g_reg[i] = g_reg[--g_reg_n];
+        }
+        break;
       }
     pthread_mutex_unlock(&g_pool_mu);
   }
-  if (bytes >= POOL_MIN_BYTES) return big_alloc(bytes);
-  void *p = NULL;
-  return posix_memalign(&p, 4096, bytes ? bytes : 1) ? NULL : p;
+  return p;
 }
 
+/* Return a buffer of a `bytes` request (the class is recomputed). */
 static void pool_give(void *p, size_t bytes) {
   if (!p) return;
-  if (bytes >= POOL_MIN_BYTES) {
-    pthread_mutex_lock(&g_pool_mu);
-    if (g_pool_n < POOL_SLOTS && g_pool_bytes + bytes <= g_pool_cap) {
-      g_pool[g_pool_n].p = p;
-      g_pool[g_pool_n].bytes = bytes;
-      g_pool_n++;
-      g_pool_bytes += bytes;
-      p = NULL;
-    }
-    pthread_mutex_unlock(&g_pool_mu);
+  if (bytes < POOL_MIN_BYTES) {
+    free(p);
+    return;
   }
-  big_free(p, bytes);
+  const size_t cls = pool_class(bytes);
+  void *evict[POOL_SLOTS];
+  size_t evict_b[POOL_SLOTS];
+  int ne = 0;
+  pthread_once(&g_pool_once, pool_caps);
+  pthread_mutex_lock(&g_pool_mu);
+  if (cls <= g_pool_cap) {
+    /* make room: the least recently returned buffers go */
+    while (g_pool_n > 0 && (g_pool_n >= POOL_SLOTS || g_pool_bytes + cls > g_pool_cap)) {
+      int old = 0;
+      for (int i = 1; i < g_pool_n; ++i)
+        if (g_pool[i].stamp < g_pool[old].stamp) old = i;
+      evict[ne] = g_pool[old].p;
+      evict_b[ne++] = g_pool[old].bytes;
+      g_pool_bytes -= g_pool[old].bytes;
+      g_pool[old] = g_pool[--g_pool_n];
+    }
+    g_pool[g_pool_n].p = p;
+    g_pool[g_pool_n].bytes = cls;
+    g_pool[g_pool_n].stamp = ++g_pool_clock;
+    g_pool_n++;
+    g_pool_bytes += cls;
+    p = NULL;
+  }
+  pthread_mutex_unlock(&g_pool_mu);
+  for (int i = 0; i < ne; ++i) big_free(evict[i], evict_b[i]);
+  if (p) big_free(p, cls);
+}
+
+/* Pool state for the tests: buffers, bytes, page-locked buffers, bytes. */
+static napi_value js_pool_stats(napi_env env, napi_callback_info info) {
+  (void)info;
+  pthread_mutex_lock(&g_pool_mu);
+  const double v[4] = {(double)g_pool_n, (double)g_pool_bytes, (double)g_reg_n, (double)g_reg_bytes};
+  pthread_mutex_unlock(&g_pool_mu);
+  napi_value arr;
+  NAPI_CALL(env, napi_create_array_with_length(env, 4, &arr));
+  for (uint32_t i = 0; i < 4; ++i) {
+    napi_value x;
+    NAPI_CALL(env, napi_create_double(env, v[i], &x));
+    NAPI_CALL(env, napi_set_element(env, arr, i, x));
+  }
+  return arr;
 }
 
 static void pool_finalize(napi_env env, void *data, void *hint) {
@@ -959,6 +1057,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"setRefineParams", 0, js_refine_params, 0, 0, 0, napi_enumerable, 0},
       {"detect", 0, js_detect, 0, 0, 0, napi_enumerable, 0},
       {"detectAsync", 0, js_detect_async, 0, 0, 0, napi_enumerable, 0},
+      {"poolStats", 0, js_pool_stats, 0, 0, 0, napi_enumerable, 0},
       {"detectBatch", 0, js_detect_batch, 0, 0, 0, napi_enumerable, 0},
       {"counts", 0, js_counts, 0, 0, 0, napi_enumerable, 0},
       {"timings", 0, js_timings, 0, 0, 0, napi_enumerable, 0},

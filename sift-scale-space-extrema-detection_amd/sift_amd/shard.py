@@ -520,14 +520,20 @@ def side_group(group=None):
     would hold back the base all-gather every tail octave waits for; on its
     own communicator it runs beside the base gather and the tail octaves."""
     import torch.distributed as dist
+    # The cache holds the group object it was made for (so its id cannot be
+    # reused while cached) and, for the default world, the world group of the
+    # time: a destroy_process_group / init_process_group cycle makes a new
+    # world, and the stale side communicator is dropped, not reused.
+    owner = group if group is not None else dist.distributed_c10d._get_default_group()
     key = id(group) if group is not None else None
-    g = _SIDE_GROUPS.get(key)
-    if g is None:
-        if group is None:
-            g = dist.new_group()
-        else:  # only the group's ranks call this
-            g = dist.new_group(ranks=dist.get_process_group_ranks(group), use_local_synchronization=True)
-        _SIDE_GROUPS[key] = g
+    ent = _SIDE_GROUPS.get(key)
+    if ent is not None and ent[0] is owner:
+        return ent[1]
+    if group is None:
+        g = dist.new_group()
+    else:  # only the group's ranks call this
+        g = dist.new_group(ranks=dist.get_process_group_ranks(group), use_local_synchronization=True)
+    _SIDE_GROUPS[key] = (owner, g)
     return g
 
 

@@ -92,3 +92,42 @@ def test_shard_images_covers_batch_once():
         for r in range(world):
             seen += shard_images(n, world, r)
         assert seen == list(range(n))
+
+
+def _side_worker(rank, world, ports, out_q):
+    from sift_amd import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    res = []
+    for port in ports:  # two process-group lifetimes in one process
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            g1 = shard.side_group()
+            g2 = shard.side_group()
+            t = torch.tensor([rank + 1.0])
+            dist.all_reduce(t, group=g1)
+            res.append((id(g1), g1 is g2, float(t.item())))
+        finally:
+            dist.destroy_process_group()
+    out_q.put((rank, res))
+
+
+def test_side_group_survives_process_group_reinit():
+    """the side communicator cached for the default world is made
+    again after destroy_process_group / init_process_group (a stale one would
+    error or hang), and reused within one lifetime."""
+    world = 2
+    ports = [_free_port(), _free_port()]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_side_worker, args=(r, world, ports, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        (a_id, a_same, a_sum), (b_id, b_same, b_sum) = results[r]
+        assert a_same and b_same            # cached within a lifetime
+        assert a_sum == b_sum == 3.0        # the second lifetime's side group works

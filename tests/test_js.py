@@ -188,3 +188,25 @@ def test_js_worker_message_stream_matches_reference(name):
             diff_px += int((d > 0).sum())
             total += n
     assert diff_px <= 1e-3 * total, (diff_px, total)
+
+
+@pytest.mark.gpu
+def test_js_result_pool_reuse_eviction_and_pinned_cap():
+    """the addon's result pool takes, returns, page-locks and
+    evicts real buffers (planes of >= 1 MiB), within its byte and pinned caps,
+    and a reused buffer holds the new values."""
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "o.json")
+        env = dict(os.environ, SIFT_NAPI_POOL_MB="24", SIFT_NAPI_PIN_MB="8")
+        r = subprocess.run([NODE, "--expose-gc", os.path.join(ROOT, "tests", "js", "run_pool.mjs"), out],
+                           capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr
+        with open(out) as f:
+            o = json.load(f)
+    mb = 1 << 20
+    assert o["afterGc"]["buffers"] > 0                       # collected planes came back
+    assert o["reuse"]["pinned"] > 0                          # first reuse page-locks
+    assert o["sameValues"] and o["sameValuesAgain"]
+    for k in ("before", "afterGc", "reuse", "afterSecondGc", "final"):
+        assert o[k]["bytes"] <= 24 * mb                      # eviction keeps the pool within its cap
+        assert o[k]["pinnedBytes"] <= 8 * mb                 # and the page-locked bytes within theirs
