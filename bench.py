@@ -198,8 +198,9 @@ def main():
                          "detections per step")
     ap.add_argument("--inflight", type=int, default=None,
                     help="detections in flight per GPU (one context each; the host settles image k while "
-                         "image k+1 runs).  Default: 2 for single images (4K: 2 > 3 by 1.5-2 %%, "
-                         "profiles/r4am_inflight_ab.txt), 3 for batched launches (cfg 4: 3 > 2 by 3 %%, DESIGN 8a)")
+                         "image k+1 runs).  Default: 2 for single images of >= 4 Mpix (4K: 2 > 3 by 1.5-2 %%, "
+                         "profiles/r4am_inflight_ab.txt), 3 for smaller ones (1080p: +15 %%, "
+                         "profiles/r5h_cfg2_inflight.txt) and for batched launches (cfg 4: 3 > 2 by 3 %%, DESIGN 8a)")
     ap.add_argument("--overlap", default="octave0",
                     choices=["none", "octave0", "gaussian", "refinement", "full", "phased"],
                     help="how consecutive images overlap on the GPU: none = contexts share one stream; "
@@ -266,7 +267,11 @@ def main():
         d_imgs = torch.from_numpy(np.stack([img] + [blob_image(W, H, seed=1000 + 64 * rank + i)
                                                    for i in range(1, Bt)])).to("cuda:%d" % dev)
     torch.cuda.synchronize(dev)
-    nin = max(1, args.inflight if args.inflight is not None else (3 if args.batch > 1 else 2))
+    # in flight: 2 for single 4K images (2 > 3 by 1.5-2 %, profiles/r4am_inflight_ab.txt), 3 for batched
+    # launches and for single images up to ~1080p (1080p: 5.20 / 5.96 / 5.10 Gpix/s at 2 / 3 / 4,
+    # profiles/r5h_cfg2_inflight.txt: a small image leaves the chip room for a third)
+    nin = max(1, args.inflight if args.inflight is not None else
+              (3 if args.batch > 1 or W * H < 4000000 else 2))
     ctxs = [sift_amd.Context(dev)]
     own = args.overlap != "none"
     after = {"octave0": sift_amd.AFTER_OCTAVE0, "gaussian": sift_amd.AFTER_GAUSSIAN,

@@ -28,33 +28,36 @@ const opts = (img) => ({ input_image: img, number_of_octaves: 3, scales_per_octa
 async function settle() {
   for (let i = 0; i < 3; i++) { global.gc(); await new Promise((r) => setImmediate(r)); }
 }
-const out = {};
-const img = blobs(7);
-let ss = sift.computeGaussianScaleSpace(opts(img));
-let dog = sift.computeDifferenceOfGaussians(ss);
-const first = sums(ss).concat(sums(dog));
-out.before = sift.poolStats();
-ss = null; dog = null;
-await settle();
-out.afterGc = sift.poolStats();
-// the same chain again: its planes come from the pool (first reuse page-locks them)
-ss = sift.computeGaussianScaleSpace(opts(img));
-dog = sift.computeDifferenceOfGaussians(ss);
-const second = sums(ss).concat(sums(dog));
-out.reuse = sift.poolStats();
-out.sameValues = JSON.stringify(first) === JSON.stringify(second);
-// a third chain while the second is alive, then both collected: more than the
-// pool cap comes back, the oldest buffers are evicted
-const ss3 = sift.computeGaussianScaleSpace(opts(blobs(8)));
-const dog3 = sift.computeDifferenceOfGaussians(ss3);
-out.third = sums(ss3).length + sums(dog3).length;
-ss = null; dog = null;
-await settle();
-out.afterSecondGc = sift.poolStats();
-// reused buffers hold the new values, page-locked or not
-const ss4 = sift.computeGaussianScaleSpace(opts(img));
-out.sameValuesAgain = JSON.stringify(sums(ss4)) === JSON.stringify(first.slice(0, 3));
-out.final = sift.poolStats();
-out.poolCapMB = Number(process.env.SIFT_NAPI_POOL_MB || 0);
-out.pinCapMB = Number(process.env.SIFT_NAPI_PIN_MB || 0);
-fs.writeFileSync(outPath, JSON.stringify(out));
+async function main() {
+  const out = {};
+  const img = blobs(7);
+  let ss = sift.computeGaussianScaleSpace(opts(img));
+  let dog = sift.computeDifferenceOfGaussians(ss);
+  const first = sums(ss).concat(sums(dog));
+  out.before = sift.poolStats();
+  ss = null; dog = null;
+  await settle();
+  out.afterGc = sift.poolStats();
+  // the same chain again: its planes come from the pool (first reuse page-locks them)
+  ss = sift.computeGaussianScaleSpace(opts(img));
+  dog = sift.computeDifferenceOfGaussians(ss);
+  const second = sums(ss).concat(sums(dog));
+  out.reuse = sift.poolStats();
+  out.sameValues = JSON.stringify(first) === JSON.stringify(second);
+  // a third chain while the second is alive, then both collected: more than the
+  // pool cap comes back, the oldest buffers are evicted
+  const ss3 = sift.computeGaussianScaleSpace(opts(blobs(8)));
+  const dog3 = sift.computeDifferenceOfGaussians(ss3);
+  out.third = sums(ss3).length + sums(dog3).length;
+  ss = null; dog = null;
+  await settle();
+  out.afterSecondGc = sift.poolStats();
+  // reused buffers hold the new values, page-locked or not
+  const ss4 = sift.computeGaussianScaleSpace(opts(img));
+  out.sameValuesAgain = JSON.stringify(sums(ss4)) === JSON.stringify(first.slice(0, 3));
+  out.final = sift.poolStats();
+  out.poolCapMB = Number(process.env.SIFT_NAPI_POOL_MB || 0);
+  out.pinCapMB = Number(process.env.SIFT_NAPI_PIN_MB || 0);
+  fs.writeFileSync(outPath, JSON.stringify(out));
+}
+main().catch((e) => { console.error(e); process.exit(1); });
