@@ -498,7 +498,8 @@ def main():
                                "context" % nin)),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "Gaussian+DoG pass: k_gauss_dog, %d launches (one per octave%s)" %
+                "kernel": "Gaussian+DoG pass: every launch of one image's %d octaves%s (4K O4 S5: k_gauss_dog for "
+                          "octaves 0 and 2, k_gauss_rw for octave 1, k_gauss_vert + k_gauss_dog for octave 3)" %
                           (O, ", each over the batch of %d images" % Bt if batched else ""),
                 "achieved": round(gbs(B, iso_pass), 1),
                 "peak": HBM_PEAK_GBS,
