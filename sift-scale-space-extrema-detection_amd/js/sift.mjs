@@ -643,6 +643,37 @@ export function createWorkerHandler(post, { matrix2d = true, device = 0, preview
   };
 }
 
+// Hand results back early: every Gaussian / DoG plane of the given scale
+// spaces (as computeGaussianScaleSpace / computeDifferenceOfGaussians return
+// them) and every typed keypoint field (format 'typed') that lives in one of
+// the addon's recycled buffers is detached and its memory returned at once, so
+// the next call of the same geometry reads its planes into those (page-locked)
+// buffers instead of fresh pages (planes of a 4K pyramid: 2.6 GB per chain).
+// Opt-in, for callers that run the chain repeatedly (frames of a video):
+// released arrays read as empty afterwards.  Returns the buffers released.
+export function release(...results) {
+  let n = 0;
+  const seen = new Set();
+  const visit = (v, depth) => {
+    if (!v || typeof v !== 'object' || depth > 4) return;
+    if (ArrayBuffer.isView(v)) {
+      if (!seen.has(v.buffer)) {
+        seen.add(v.buffer);
+        if (native.releaseBuffer(v.buffer)) n++;
+      }
+      return;
+    }
+    if (Array.isArray(v)) {
+      if (v.length && typeof v[0] !== 'object') return;  // a Matrix2D row or a number list
+      for (const x of v) visit(x, depth + 1);
+      return;
+    }
+    for (const k of ['image', 'data', 'ints', 'doubles']) if (k in v) visit(v[k], depth + 1);
+  };
+  for (const r of results) visit(r, 0);
+  return n;
+}
+
 // The addon's recycled result buffers (>= 1 MiB planes and keypoint
 // fields): buffers and bytes held for reuse, buffers and bytes page-locked.
 export function poolStats() {

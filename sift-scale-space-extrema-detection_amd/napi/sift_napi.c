@@ -10,7 +10,7 @@
  * Promise, so the JS thread is not blocked -- the role the reference's Web
  * Worker plays.
  */
-#define NAPI_VERSION 6
+#define NAPI_VERSION 7  /* napi_detach_arraybuffer (releaseBuffer); Node >= 12.16 */
 #include <node_api.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -334,23 +334,74 @@ static napi_value js_pool_stats(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+/* One external ArrayBuffer over a pool buffer.  `released`: the caller handed
+ * it back early (releaseBuffer: detached, returned to the pool); the
+ * finalizer then only frees the record. */
+typedef struct {
+  void *p;
+  size_t bytes;
+  int released;
+} pool_rec;
+
 static void pool_finalize(napi_env env, void *data, void *hint) {
-  const size_t bytes = (size_t)(uintptr_t)hint;
-  int64_t adj;
-  napi_adjust_external_memory(env, -(int64_t)bytes, &adj);
-  pool_give(data, bytes);
+  (void)data;
+  pool_rec *r = (pool_rec *)hint;
+  if (!r->released) {
+    int64_t adj;
+    napi_adjust_external_memory(env, -(int64_t)r->bytes, &adj);
+    pool_give(r->p, r->bytes);
+  }
+  free(r);
 }
 
 /* An external ArrayBuffer over a pool buffer (takes ownership of p, also on failure). */
 static napi_value pool_arraybuffer(napi_env env, void *p, size_t bytes) {
   napi_value ab;
-  if (napi_create_external_arraybuffer(env, p, bytes, pool_finalize, (void *)(uintptr_t)bytes, &ab) != napi_ok) {
+  pool_rec *r = (pool_rec *)malloc(sizeof(pool_rec));
+  if (!r) {
     pool_give(p, bytes);
     return NULL;
   }
+  r->p = p;
+  r->bytes = bytes;
+  r->released = 0;
+  if (napi_create_external_arraybuffer(env, p, bytes, pool_finalize, r, &ab) != napi_ok) {
+    free(r);
+    pool_give(p, bytes);
+    return NULL;
+  }
+  /* the record travels with the object: releaseBuffer finds it */
+  if (napi_wrap(env, ab, r, NULL, NULL, NULL) != napi_ok) r->released = -1; /* not releasable early */
   int64_t adj;
   napi_adjust_external_memory(env, (int64_t)bytes, &adj);
   return ab;
+}
+
+/* releaseBuffer(arrayBuffer) -> bool: hand a pooled result buffer (a plane or
+ * a typed keypoint field of >= 1 MiB) back before V8 collects it: the
+ * ArrayBuffer is detached (its views read as empty from then on) and the
+ * memory returns to the pool at once, so the next result of its size class
+ * reuses it -- page-locked on reuse -- instead of faulting in fresh pages.
+ * false for any other buffer (left untouched). */
+static napi_value js_release_buffer(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], res;
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bool ok = false, isab = false;
+  void *w = NULL;
+  if (argc > 0 && napi_is_arraybuffer(env, argv[0], &isab) == napi_ok && isab &&
+      napi_unwrap(env, argv[0], &w) == napi_ok && w) {
+    pool_rec *r = (pool_rec *)w;
+    if (r->released == 0 && napi_detach_arraybuffer(env, argv[0]) == napi_ok) {
+      r->released = 1;
+      int64_t adj;
+      napi_adjust_external_memory(env, -(int64_t)r->bytes, &adj);
+      pool_give(r->p, r->bytes);
+      ok = true;
+    }
+  }
+  NAPI_CALL(env, napi_get_boolean(env, ok, &res));
+  return res;
 }
 
 /* make_typed over a recycled buffer (large results). */
@@ -1058,6 +1109,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"detect", 0, js_detect, 0, 0, 0, napi_enumerable, 0},
       {"detectAsync", 0, js_detect_async, 0, 0, 0, napi_enumerable, 0},
       {"poolStats", 0, js_pool_stats, 0, 0, 0, napi_enumerable, 0},
+      {"releaseBuffer", 0, js_release_buffer, 0, 0, 0, napi_enumerable, 0},
       {"detectBatch", 0, js_detect_batch, 0, 0, 0, napi_enumerable, 0},
       {"counts", 0, js_counts, 0, 0, 0, napi_enumerable, 0},
       {"timings", 0, js_timings, 0, 0, 0, napi_enumerable, 0},

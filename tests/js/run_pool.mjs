@@ -56,6 +56,15 @@ async function main() {
   const ss4 = sift.computeGaussianScaleSpace(opts(img));
   out.sameValuesAgain = JSON.stringify(sums(ss4)) === JSON.stringify(first.slice(0, 3));
   out.final = sift.poolStats();
+  // handed back early: detached at once, their memory back in the pool
+  const before = sift.poolStats().buffers;
+  out.released = sift.release(ss4);
+  out.detached = ss4[0][0].image.data.length === 0;
+  out.afterRelease = sift.poolStats();
+  out.releasedIntoPool = out.afterRelease.buffers > before || out.afterRelease.bytes >= 0;
+  out.releaseAgain = sift.release(ss4);  // already released: nothing
+  const ss5 = sift.computeGaussianScaleSpace(opts(img));
+  out.sameValuesAfterRelease = JSON.stringify(sums(ss5)) === JSON.stringify(first.slice(0, 3));
   out.poolCapMB = Number(process.env.SIFT_NAPI_POOL_MB || 0);
   out.pinCapMB = Number(process.env.SIFT_NAPI_PIN_MB || 0);
   fs.writeFileSync(outPath, JSON.stringify(out));

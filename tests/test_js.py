@@ -207,6 +207,8 @@ def test_js_result_pool_reuse_eviction_and_pinned_cap():
     assert o["afterGc"]["buffers"] > 0                       # collected planes came back
     assert o["reuse"]["pinned"] > 0                          # first reuse page-locks
     assert o["sameValues"] and o["sameValuesAgain"]
-    for k in ("before", "afterGc", "reuse", "afterSecondGc", "final"):
+    assert o["released"] > 0 and o["detached"] and o["releaseAgain"] == 0   # sift.release: detach + return
+    assert o["sameValuesAfterRelease"]
+    for k in ("before", "afterGc", "reuse", "afterSecondGc", "final", "afterRelease"):
         assert o[k]["bytes"] <= 24 * mb                      # eviction keeps the pool within its cap
         assert o[k]["pinnedBytes"] <= 8 * mb                 # and the page-locked bytes within theirs

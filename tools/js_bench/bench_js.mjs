@@ -93,6 +93,28 @@ out.detectAsync = {
   }
 }
 
+// 2c. detectAsync with keypoint objects as a server consumes them: up to 3
+// images in flight, each result taken in order and dropped (Promise.all above
+// keeps all of them alive at once: the GC then walks every image's 445 K
+// objects at each collection)
+{
+  const nq = Math.max(3 * reps, 12), depth = 3;
+  for (let i = 0; i < 3; i++) await sift.detectAsync(image, opts);
+  const t0 = performance.now();
+  const q = [];
+  let nkp = 0;
+  for (let i = 0; i < nq; i++) {
+    q.push(sift.detectAsync(image, opts));
+    if (q.length === depth) nkp = (await q.shift()).length;
+  }
+  while (q.length) nkp = (await q.shift()).length;
+  const ms = performance.now() - t0;
+  out.detectAsync_objects_stream = {
+    keypoints: nkp, images: nq, total_ms: ms, ms_per_image: ms / nq, mpix_per_s: nq * mpix / (ms / 1e3),
+    what: `${nq} detectAsync(image) (keypoint objects), ${depth} in flight, each result awaited in order and dropped`,
+  };
+}
+
 // 3. the reference's four stages on host arrays (ImageData-shaped planes)
 const stages = { gauss: [], dog: [], find: [], refine: [] };
 let nc = 0, nk = 0;
@@ -136,6 +158,36 @@ out.stages = {
     + 'ImageData-shaped Float32Array (the reference returns them), candidates and keypoints as JS objects; '
     + 'the device pyramid stays resident between stages',
 };
+// 3b. the same chain, each iteration's planes handed back (sift.release)
+// before the next: the planes are read into the recycled page-locked buffers
+{
+  const st2 = { gauss: [], dog: [] };
+  const it = Math.max(3, Math.min(reps, 6));
+  for (let i = 0; i < it; i++) {
+    let t0 = performance.now();
+    const ss = sift.computeGaussianScaleSpace({ input_image: image, ...opts });
+    const tg = performance.now() - t0;
+    t0 = performance.now();
+    const dog = sift.computeDifferenceOfGaussians(ss);
+    const td = performance.now() - t0;
+    const cands = sift.findCandidateKeypoints({ differenceOfGaussians: dog, scalesPerOctave: S });
+    sift.refineCandidateKeypoints({ differenceOfGaussians: dog, scalesPerOctave: S, numberOfOctaves: O,
+      candidateKeypoints: cands, minBlurLevel: 0.8, minInterpixelDistance: 0.5 });
+    if (i > 0) { st2.gauss.push(tg); st2.dog.push(td); }  // the first iteration fills the pool
+    sift.release(ss, dog);
+  }
+  const gaussBytes = planeBytes - dogBytes;
+  out.stages_released = {
+    computeGaussianScaleSpace_ms: med(st2.gauss), computeDifferenceOfGaussians_ms: med(st2.dog),
+    planes_to_host_bytes: planeBytes,
+    planes_gb_per_s: planeBytes / ((med(st2.gauss) + med(st2.dog)) / 1e3) / 1e9,
+    gauss_stage_gb_per_s: gaussBytes / (med(st2.gauss) / 1e3) / 1e9,
+    dog_stage_read_gb_per_s: dogBytes / (med(st2.dog) / 1e3) / 1e9,
+    pool: sift.poolStats(),
+    what: 'the chain\'s first two stages with the previous iteration\'s planes handed back (sift.release(ss, dog)): '
+      + 'every plane is one DMA into a recycled page-locked buffer; medians over the iterations after the first',
+  };
+}
 fs.writeFileSync(outPath, JSON.stringify(out, null, 1));
 console.log(JSON.stringify(out));
 }
