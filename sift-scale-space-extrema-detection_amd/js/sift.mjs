@@ -446,7 +446,7 @@ function asyncPool(st, inflight) {
   return st.pool;
 }
 
-function release(pool, slot) {
+function releaseSlot(pool, slot) {
   const i = pool.waiters.findIndex((w) => pool.ctxs.indexOf(slot) < w.limit);
   if (i >= 0) {
     const [w] = pool.waiters.splice(i, 1);
@@ -474,15 +474,15 @@ export function detectAsync(input_image, opts = {}) {
       if (slot.ctx === st.ctx) bump(st, 'detecting', img.width, img.height, params);
       job = native.detectAsync(slot.ctx, img.data, img.width, img.height, params);
     } catch (e) {
-      release(pool, slot);
+      releaseSlot(pool, slot);
       return Promise.reject(e);
     }
     return job.then((r) => {
-      release(pool, slot);
+      releaseSlot(pool, slot);
       st.lastCtx = slot.ctx;
       return keypointsOut(r, format);
     }, (e) => {
-      release(pool, slot);
+      releaseSlot(pool, slot);
       throw e;
     });
   };
