@@ -1284,6 +1284,9 @@ __host__ __device__ constexpr int rw_row(int t) { return t * kRwSW + 2 * (t >> 2
 #ifndef SIFT_RWTAPS
 #define SIFT_RWTAPS 8  // taps per reload of the tap pointer (0: never: the compiler keeps them in SGPRs)
 #endif
+#ifndef SIFT_RWS_DEFAULT
+#define SIFT_RWS_DEFAULT 1  // streamed k_gauss_rw for radii 13..24 (gauss_rws; profiles/r5k_streamed_rw_ab.txt)
+#endif
 #ifndef SIFT_RW_WPE
 #define SIFT_RW_WPE 1  // minimum waves per SIMD the register allocation must allow
 #endif
@@ -1387,7 +1390,31 @@ __device__ __forceinline__ void rw_horz_epi_(std::integer_sequence<int, Rs...>, 
    ...);
 }
 
-template <int RW>
+// Streamed vertical pass of one strip column (k_gauss_rw<RW, true>): the
+// scale's own window rows y0 - r .. y0 + 7 + r loaded per scale from the base
+// plane (L2-resident for the mid-radius octaves: XCD-banded tiles), in
+// vert_glob_gen's 8-row chunks over zero-padded taps -- the same fma chain per
+// output as the register window, bit for bit.
+__device__ __forceinline__ void rw_vert_stream(__amdgpu_buffer_rsrc_t rs, int xoff, int y0, int h, int w, int r,
+                                               const cdouble* wp, double (&acc)[8]) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+  const int yb = y0 - r, NJ = 2 * r + 8;
+  auto chunk = [&](int jb, auto C, auto first) {
+    using CC = decltype(C);
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < CC::kRows; ++k)
+      v[k] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(yb + jb + k, 0, h - 1) * w * 8));
+    const cdouble* wq = wp + jb;
+    CC::template run<decltype(first)::value>([&](int k, int t) { acc[t] = fma((double)wq[k - t], v[k], acc[t]); });
+    pin(acc);
+  };
+  vchunk_dispatch<true>(2 * r, [&](auto C, auto f) { chunk(0, C, f); });
+  for (int jb = 8; jb < NJ; jb += 8) vchunk_dispatch<false>(2 * r - jb, [&](auto C, auto f) { chunk(jb, C, f); });
+}
+
+template <int RW, bool STREAM = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE))) void k_gauss_rw(const Pyramid P, const GaussLaunch L) {
   using G = RwGeom<RW>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1411,14 +1438,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
   const int x0 = bx * G::TW, y0 = by * kRwRows;
   const int c = threadIdx.x;  // strip column
   // The lane's base window: rows y0 - RW .. y0 + 7 + RW of image column x0 - RW + c (clamped).
-  double win[G::NW];
-  {
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
-    const int xoff = clampi(x0 - RW + c, 0, w - 1) * 8;
+  const __amdgpu_buffer_rsrc_t brs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
+  const int bxoff = clampi(x0 - RW + c, 0, w - 1) * 8;
+  double win[STREAM ? 1 : G::NW];
+  if constexpr (!STREAM) {
 #pragma unroll
     for (int j = 0; j < G::NW; ++j)
-      win[j] = load_f64(rs, xoff, __builtin_amdgcn_readfirstlane(clampi(y0 - RW + j, 0, h - 1) * w * 8));
+      win[j] = load_f64(brs, bxoff, __builtin_amdgcn_readfirstlane(clampi(y0 - RW + j, 0, h - 1) * w * 8));
   }
   // Horizontal items of 4 columns x 2 rows: ds_read_b128 lane group gid =
   // 4 wv + g (b128_group) at position j: column group cg = 8 (gid >> 1) +
@@ -1448,7 +1475,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
     double* Vs = smem + (s & 1) * kRwStrip;
     {
       double acc[8];
-      rw_vert_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, r, win, wp, acc);
+      if constexpr (STREAM) {
+        int xo = bxoff;
+        asm volatile("" : "+v"(xo));  // per-scale opaque: no hoisted per-radius addresses
+        rw_vert_stream(brs, xo, y0, h, w, r, wp, acc);
+      } else {
+        rw_vert_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, r, win, wp, acc);
+      }
 #pragma unroll
       for (int t = 0; t < 8; ++t) Vs[rw_row(t) + c] = acc[t];
     }
@@ -1505,11 +1538,26 @@ static int rw_width(const Pyramid& P, int o) {
   return R <= 12 ? 12 : R <= 16 ? 16 : R <= 24 ? 24 : 0;
 }
 
+// Octaves >= 1 whose radii exceed the register window (SIFT_RW_R) up to 24
+// run k_gauss_rw with the streamed vertical pass (rw_vert_stream): 208-column
+// tiles in a 256-column strip instead of k_gauss_dog's 64-column tiles with
+// (64 + 2r) / 64 of the vertical work (SIFT_RWS=0: k_gauss_dog, A/B builds).
+// SIFT_RWS bit 0: radii 13..24; bit 1: also the register-window octaves
+// (radii <= 12) streamed.
+static bool gauss_rws(const Pyramid& P, int o) {
+  static const int on = exp_knob("SIFT_RWS", SIFT_RWS_DEFAULT);
+  static const int rlim = exp_knob("SIFT_RW_R", 12);
+  const int r = P.oct[o].rmax;
+  if (!on || o < 1 || P.oct[o].w < 2 || r > 24 || gauss_keep_l64(P, o)) return false;
+  return r > std::min(rlim, 24) ? (on & 1) != 0 : (on & 2) != 0;
+}
+
 bool gauss_wide(const Pyramid& P, int o) {
   static const int on = exp_knob("SIFT_RW", 1);
   static const int rlim = exp_knob("SIFT_RW_R", 12);
-  return on && o >= 1 && P.oct[o].w >= 2 && P.oct[o].rmax <= std::min(rlim, 24) && rw_width(P, o) > 0 &&
-         !gauss_keep_l64(P, o);
+  return (on && o >= 1 && P.oct[o].w >= 2 && P.oct[o].rmax <= std::min(rlim, 24) && rw_width(P, o) > 0 &&
+          !gauss_keep_l64(P, o)) ||
+         gauss_rws(P, o);
 }
 
 static int rw_tile_w(const Pyramid& P, int o) { return rw_width(P, o) <= 16 ? 224 : 192; }
@@ -1795,7 +1843,9 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     L.zero = 0;
     const dim3 grid(L.gx * L.gy * L.G * L.nimg);
     const size_t lds = occupancy_lds(L.o, rw_lds(P, L.o));
-    if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
+    if (gauss_rws(P, L.o) && RW == 12) hipLaunchKernelGGL((k_gauss_rw<12, true>), grid, dim3(256), lds, st, P, L);
+    else if (gauss_rws(P, L.o)) hipLaunchKernelGGL((k_gauss_rw<24, true>), grid, dim3(256), lds, st, P, L);
+    else if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
     else if (RW == 16) hipLaunchKernelGGL(k_gauss_rw<16>, grid, dim3(256), lds, st, P, L);
     else hipLaunchKernelGGL(k_gauss_rw<24>, grid, dim3(256), lds, st, P, L);
     return hipGetLastError();
