@@ -1843,7 +1843,9 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     L.zero = 0;
     const dim3 grid(L.gx * L.gy * L.G * L.nimg);
     const size_t lds = occupancy_lds(L.o, rw_lds(P, L.o));
+    // (the streamed kernels use the tile geometry of their RW, as the window ones)
     if (gauss_rws(P, L.o) && RW == 12) hipLaunchKernelGGL((k_gauss_rw<12, true>), grid, dim3(256), lds, st, P, L);
+    else if (gauss_rws(P, L.o) && RW == 16) hipLaunchKernelGGL((k_gauss_rw<16, true>), grid, dim3(256), lds, st, P, L);
     else if (gauss_rws(P, L.o)) hipLaunchKernelGGL((k_gauss_rw<24, true>), grid, dim3(256), lds, st, P, L);
     else if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
     else if (RW == 16) hipLaunchKernelGGL(k_gauss_rw<16>, grid, dim3(256), lds, st, P, L);

@@ -144,7 +144,7 @@ def test_cfg5_8k_o6_s5_matches_oracle(gpu_ctx, img8k, mode):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("W,H,O,S,seed", [(640, 480, 5, 5, 3), (333, 517, 4, 3, 4), (1920, 1080, 4, 5, 42),
-                                         (3840, 2160, 4, 5, 42)])
+                                         (3840, 2160, 4, 5, 42), (1280, 720, 3, 3, 5)])
 def test_planes_bit_exact_in_gpu_order(gpu_ctx, W, H, O, S, seed):
     """Every Gaussian and DoG plane is the fp32 rounding of the oracle's fp64
     value computed in the HIP path's operation order, bit for bit."""
