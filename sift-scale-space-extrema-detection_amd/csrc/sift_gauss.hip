@@ -1702,7 +1702,7 @@ static int scale_groups(const Pyramid& P, int o) {
   }();
   if (o == 0) return 1;
   if (o - 1 < (int)env.size() && env[o - 1] > 0) return std::min(env[o - 1], P.NS);
-  // Measured (4K, O=4, S=5; tools/gpu_groups.sh): every split adds the
+  // Measured (4K, O=4, S=5; tools/experiments/gpu_groups.sh): every split adds the
   // recomputed scale to the total work, so an octave splits only until it
   // has ~1.5 blocks per CU -- 60x68 tiles: 1 group; 30x34: 1 (G=2: 116 us,
   // G=4: 126-140 us, G=1: 103 us); 15x17: 2 (70.8 us; G=1 94 us, G=4 85 us).
