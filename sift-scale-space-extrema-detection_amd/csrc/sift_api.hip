@@ -164,6 +164,7 @@ struct sift_ctx {
   bool x_words = false;                        // this extrema stage lists ambiguous words, not keys
   DBuf cand_key, cand_val, cand_keep;          // ordered candidates
   DBuf patch, wslot, cand_patch;               // first-step patches captured by the scan (ExtremaLaunch.patch)
+  DBuf pre;                                    // the scan's first refinement steps (ExtremaLaunch.pre, SIFT_XREFINE)
   bool x_patch = false;                        // this extrema stage captures patches
   bool has_patch = false;                      // cand_patch indexes the current slots
   DBuf lowbitmap, lowrowcount, lowrowoff;      // low-contrast list (SIFT_F_LOW_CONTRAST_LIST)
@@ -373,7 +374,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab,
                   &ctx->lowbitmap, &ctx->lowrowcount, &ctx->lowrowoff, &ctx->low_key, &ctx->low_val,
                   &ctx->late_key, &ctx->late_val, &ctx->band_cnt, &ctx->band_first, &ctx->band_start,
-                  &ctx->perm, &ctx->patch, &ctx->wslot, &ctx->cand_patch};
+                  &ctx->perm, &ctx->patch, &ctx->wslot, &ctx->cand_patch, &ctx->pre};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -960,14 +961,24 @@ static int extrema_prepare(sift_ctx* ctx, hipStream_t st, int nf) {
   // Patch capture (SIFT_PATCH=0: the refinement gathers every step, experiments).
   static const int capture = exp_knob("SIFT_PATCH", 1);
   const size_t slots = (size_t)ni * extrema_units(P) * kPatchUnitSlots;
-  // the scan's patch stores take 32-bit byte offsets (a larger batch gathers)
-  ctx->x_patch = SIFT_XPATCH && capture != 0 && slots * kPatchFloats * sizeof(float) < ((size_t)1 << 31);
+  // the scan's patch stores take 32-bit byte offsets (a larger batch gathers);
+  // the in-scan first step (SIFT_XREFINE) runs the fast pass's fp32 bounds,
+  // so not on caller-supplied (exact) planes
+  ctx->x_patch = kXCapture && capture != 0 &&
+                 (SIFT_XREFINE == 1 ? !exact_planes : slots * kPatchFloats * sizeof(float) < ((size_t)1 << 31));
   ctx->has_patch = false;
   if (ctx->x_patch) {
-    HIPCHK(ctx->patch.ensure(std::max<size_t>(slots, 1) * kPatchFloats * sizeof(float)));
+    if (SIFT_XREFINE == 1) {
+      HIPCHK(ctx->pre.ensure(std::max<size_t>(slots, 1) * sizeof(Keypoint)));
+      L.pre = ctx->pre.as<Keypoint>();
+      L.min_blur = ctx->p.min_blur;
+      L.min_interpixel_distance = ctx->p.min_interpixel_distance;
+    } else {
+      HIPCHK(ctx->patch.ensure(std::max<size_t>(slots, 1) * kPatchFloats * sizeof(float)));
+      L.patch = ctx->patch.as<float>();
+    }
     HIPCHK(ctx->wslot.ensure((size_t)words * sizeof(unsigned)));
     HIPCHK(ctx->cand_patch.ensure((size_t)ctx->cand_cap * sizeof(unsigned)));
-    L.patch = ctx->patch.as<float>();
     L.wslot = ctx->wslot.as<unsigned>();
   }
   return SIFT_OK;
@@ -1194,7 +1205,8 @@ static int refine_enqueue(sift_ctx* ctx) {
     R.perm = nullptr;
     if (ctx->has_patch && ctx->slots_rows) {
       R.cand_patch = ctx->cand_patch.as<unsigned>();
-      R.patch = ctx->patch.as<float>();
+      if (SIFT_XREFINE == 1) R.pre = ctx->pre.as<Keypoint>();
+      else R.patch = ctx->patch.as<float>();
     }
     static const int band_order = exp_knob("SIFT_BAND_ORDER", 1);
     if (band_order && ctx->slots_rows) {

@@ -27,6 +27,7 @@
 #include "sift_exact.h"
 #include "sift_kernels.h"
 #include "sift_xmask.h"
+#include "sift_refine.h"
 
 #ifndef SIFT_XLOAD_AUX
 #define SIFT_XLOAD_AUX 0  // cache-policy bits of the scan's DoG loads (gfx950: 1 sc0, 2 nt, 16 sc1)
@@ -52,6 +53,9 @@ struct XUnit {
   unsigned low;
   unsigned pbase, pcount;  // patch capture: the unit's first slot, slots taken
   __amdgpu_buffer_rsrc_t prsrc;  // the patch buffer (< 4 GiB: extrema_prepare checks)
+  float* cap;          // SIFT_XREFINE: this wave's capture slots in LDS
+  unsigned capa;       // ... their LDS byte address
+  bool capture;        // patches are captured (L.patch or L.pre)
   long long word0;     // index of (s_first, row 0, word 0) in L.bitmap (ambiguous word list)
 };
 
@@ -82,39 +86,55 @@ __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int
 // unit (a wave-uniform count: no atomics -- one global counter serialised
 // ~600 K atomics at the L2, 0.42 -> 6.8 ms).  Returns the slot of the first
 // one (~0u: the unit is out of slots, these candidates gather in the refinement).
+// SIFT_XREFINE: the same fields go to the wave's LDS slots (U.cap, local slot
+// numbers), field 19 = the candidate's key relative to U.key_base.
 template <int NP, int A, int B, int C>
 __device__ __forceinline__ unsigned x_capture(const XWin<NP>& Wn, XUnit<NP>& U, const ExtremaLaunch& L,
-                                              const int Q, unsigned long long b) {
+                                              const int Q, unsigned long long b, unsigned rel_key) {
   const unsigned cnt = (unsigned)__popcll(b);
   if (U.pcount + cnt > (unsigned)kPatchUnitSlots) return ~0u;
   const unsigned base = U.pbase + U.pcount;
+#if SIFT_XREFINE
+  // ds_write_b32 one value at a time (inline asm): left to itself the compiler
+  // merges the fields into b64 / b96 / b128 stores, whose consecutive source
+  // registers cost copies and ~20 VGPRs across the scan (a wave per SIMD).
+  const unsigned sa = U.capa + U.pcount * (unsigned)(kPatchFloats * 4);
+  U.pcount += cnt;
+  constexpr int kStride = kPatchFloats * 4;
+#define X_ST(v, vo, field) \
+  asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(sa + (unsigned)(vo)), "v"(v), "i"(4 * (field)))
+#else
   U.pcount += cnt;
   // Buffer stores of the window registers themselves: the slot's byte offset
   // in one VGPR, the word's first slot in an SGPR, the field in the
   // instruction's offset (16-byte or flat stores would copy each quad into
   // consecutive registers / keep 64-bit addresses: a wave per SIMD less).
   const int sb = (int)(base * (unsigned)(kPatchFloats * 4));
+  constexpr int kStride = kPatchFloats * 4;
+#define X_ST(v, voff, field) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), U.prsrc, (voff) + 4 * (field), sb, 0)
+#endif
   const int lane = U.lane;
-  auto st = [&](float v, int voff, int field) {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), U.prsrc, voff + 4 * field, sb, 0);
-  };
   if ((b >> lane) & 1ull) {  // the candidate's own column: d(k, a, 1)
-    const int vo = (int)lane_prefix(b) * (kPatchFloats * 4);
-    st(Wn.cv[A][Q - 1], vo, 0); st(Wn.cv[B][Q - 1], vo, 1); st(Wn.cv[C][Q - 1], vo, 2);
-    st(Wn.cv[A][Q], vo, 3); st(Wn.cv[B][Q], vo, 4); st(Wn.cv[C][Q], vo, 5);
-    st(Wn.cv[A][Q + 1], vo, 6); st(Wn.cv[B][Q + 1], vo, 7); st(Wn.cv[C][Q + 1], vo, 16);
+    const int vo = (int)lane_prefix(b) * kStride;
+    X_ST(Wn.cv[A][Q - 1], vo, 0); X_ST(Wn.cv[B][Q - 1], vo, 1); X_ST(Wn.cv[C][Q - 1], vo, 2);
+    X_ST(Wn.cv[A][Q], vo, 3); X_ST(Wn.cv[B][Q], vo, 4); X_ST(Wn.cv[C][Q], vo, 5);
+    X_ST(Wn.cv[A][Q + 1], vo, 6); X_ST(Wn.cv[B][Q + 1], vo, 7); X_ST(Wn.cv[C][Q + 1], vo, 16);
+#if SIFT_XREFINE
+    X_ST(__uint_as_float(rel_key), vo, 19);
+#endif
   }
   if (lane < 63 && ((b >> (lane + 1)) & 1ull)) {  // left of a candidate: d(1, a, 0), d(0, 1, 0), d(2, 1, 0)
-    const int vo = (int)lane_prefix(b >> 1) * (kPatchFloats * 4);
-    st(Wn.cv[A][Q], vo, 8); st(Wn.cv[B][Q], vo, 9); st(Wn.cv[C][Q], vo, 10);
-    st(Wn.cv[B][Q - 1], vo, 11); st(Wn.cv[B][Q + 1], vo, 17);
+    const int vo = (int)lane_prefix(b >> 1) * kStride;
+    X_ST(Wn.cv[A][Q], vo, 8); X_ST(Wn.cv[B][Q], vo, 9); X_ST(Wn.cv[C][Q], vo, 10);
+    X_ST(Wn.cv[B][Q - 1], vo, 11); X_ST(Wn.cv[B][Q + 1], vo, 17);
   }
   if (lane > 0 && ((b >> (lane - 1)) & 1ull)) {  // right of a candidate: d(1, a, 2), d(0, 1, 2), d(2, 1, 2)
-    const int vo = (int)lane_prefix(b << 1) * (kPatchFloats * 4);
-    st(Wn.cv[A][Q], vo, 12); st(Wn.cv[B][Q], vo, 13); st(Wn.cv[C][Q], vo, 14);
-    st(Wn.cv[B][Q - 1], vo, 15); st(Wn.cv[B][Q + 1], vo, 18);
+    const int vo = (int)lane_prefix(b << 1) * kStride;
+    X_ST(Wn.cv[A][Q], vo, 12); X_ST(Wn.cv[B][Q], vo, 13); X_ST(Wn.cv[C][Q], vo, 14);
+    X_ST(Wn.cv[B][Q - 1], vo, 15); X_ST(Wn.cv[B][Q + 1], vo, 18);
   }
   return base;
+#undef X_ST
 }
 
 // Centre row y (slots A = y-1, B = y, C = y+1): decide every scale of the group.
@@ -157,8 +177,8 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     }
     if (bit) {
       const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
-      if (SIFT_XPATCH && L.patch) {
-        const unsigned ps = x_capture<NP, A, B, C>(Wn, U, L, q, bit);
+      if (kXCapture && U.capture) {
+        const unsigned ps = x_capture<NP, A, B, C>(Wn, U, L, q, bit, key - U.key_base);
         if (U.lane == q - 1) wsl = ps;
       }
       if (U.lane == q - 1) {
@@ -183,7 +203,7 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
   if (U.lane < NP - 2) {
     const long long r = (long long)U.lane * U.h + y;
     U.bitmap[r * U.nw + U.xw] = ((unsigned long long)whi << 32) | wlo;
-    if (SIFT_XPATCH && L.patch && (wlo | whi)) L.wslot[U.word0 + r * U.nw + U.xw] = wsl;
+    if (kXCapture && U.capture && (wlo | whi)) L.wslot[U.word0 + r * U.nw + U.xw] = wsl;
     if (wcnt) atomicAdd(&U.rowcount[r], wcnt);
     if ((alo | ahi) && L.ambbitmap) {  // an ambiguous word (rare): its bits and its index for k_exact_words
       const long long gw = U.word0 + r * U.nw + U.xw;
@@ -199,9 +219,68 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
   }
 }
 
+#if SIFT_XREFINE
+// The first refinement step of every candidate the unit captured (lane j takes
+// slots j, j + 64, ...): refine_step on the fp32 planes with the fast pass's
+// error bounds, exactly as k_refine_fast's first iteration from a captured
+// patch; the outcome goes to pre[slot] (kPre* codes).
+template <int NP>
+__device__ __forceinline__ void x_first_steps(const Pyramid& P, const ExtremaLaunch& L, const XUnit<NP>& U) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the capture's ds_write_b32s (inline asm) have landed
+  const int o = U.o;
+  const unsigned plane = (unsigned)U.plane, w = (unsigned)U.w;
+  const int moff = (P.row0 * 2) >> o;
+  for (unsigned j = (unsigned)U.lane; j < U.pcount; j += 64) {
+    const float* pp = U.cap + j * kPatchFloats;
+    const float4 c0 = *reinterpret_cast<const float4*>(pp), c1 = *reinterpret_cast<const float4*>(pp + 4);
+    const float4 lf = *reinterpret_cast<const float4*>(pp + 8), rt = *reinterpret_cast<const float4*>(pp + 12);
+    const float4 ex = *reinterpret_cast<const float4*>(pp + 16);
+    const unsigned rel = __float_as_uint(ex.w);
+    const unsigned sq = rel / plane, rem = rel - sq * plane, mr = rem / w;
+    const int s = U.s_first + (int)sq, m = (int)mr, n = (int)(rem - mr * w);
+    const float v19[19] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w, ex.x,
+                           lf.x, lf.y, lf.z, lf.w, ex.y, rt.x, rt.y, rt.z, rt.w, ex.z};
+    constexpr int at[19] = {1, 4, 7, 10, 13, 16, 19, 22, 25, 9, 12, 15, 3, 21, 11, 14, 17, 5, 23};
+    double d[27];
+    double mx = 0;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) d[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 19; ++k) {
+      d[at[k]] = (double)v19[k];
+      mx = fmax(mx, fabs((double)v19[k]));
+    }
+    const double value = (double)c1.x;  // d(1, 1, 1)
+    const double dval = fabs(value) * 0x1p-24;
+    const double delta = mx * (0x1p-24 + 0x1p-40);
+    const StepOut R = refine_step<true>(d, o, s, m, n, value, delta, dval, P.S, P.ND, U.h, U.w, P.thr, false,
+                                        L.min_blur / L.min_interpixel_distance);
+    Keypoint k;
+    k.octave = kPreDefer;
+    if (!R.uncertain) {
+      if (R.state == 3) k.octave = kPreSingular;
+      else if (R.state == 2) k.octave = kPreDiscard;
+      else if (R.state == 1) {
+        if (!R.imprecise) {
+          make_keypoint(k, o, R, P.S, L.min_blur, L.min_interpixel_distance, moff);
+          k.octave = kPreKeep;
+        }
+      } else {
+        k.octave = kPreMoved;
+        k.scale_level = R.s;
+        k.local_y = R.m;
+        k.local_x = R.n;
+        k.interp_value = value;
+      }
+    }
+    L.pre[U.pbase + j] = k;
+  }
+}
+#endif
+
 template <int NP, bool LOWL>
 __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int b, int u, int o, int s_first,
-                                       int xw, int y0, int y1) {
+                                       int xw, int y0, int y1, float* cap) {
   const Octave& oc = P.oct[o];
   XUnit<NP> U;
   U.plane = (long long)oc.h * oc.w;
@@ -236,8 +315,11 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   U.low = 0;
   U.pbase = (unsigned)(b * L.units_per_img + u) * (unsigned)kPatchUnitSlots;
   U.pcount = 0;
+  U.capture = L.pre != nullptr || L.patch != nullptr;
   if (SIFT_XPATCH && L.patch) U.prsrc = __builtin_amdgcn_make_buffer_rsrc(L.patch, 0, -1, 0x00020000);
 
+  U.cap = cap;
+  U.capa = (unsigned)(size_t)(__attribute__((address_space(3))) float*)cap;
   XWin<NP> Wn;
   {
     float r_m1[NP], r_0[NP];
@@ -264,6 +346,18 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
     x_load(U, Wn.raw[0], min(y + 6, y1 + 1));
     x_centre<NP, 1, 2, 0, LOWL>(Wn, U, L, y + 2);
   }
+#if SIFT_XREFINE
+  if (U.capture && U.pcount) {
+    if constexpr (SIFT_XREFINE == 1) {
+      x_first_steps<NP>(P, L, U);
+    } else {  // SIFT_XREFINE=2: the LDS slots copied out whole (16-byte stores, contiguous per unit)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const float4* src = reinterpret_cast<const float4*>(U.cap);
+      float4* dst = reinterpret_cast<float4*>(L.patch + (size_t)U.pbase * kPatchFloats);
+      for (unsigned t = (unsigned)U.lane; t < U.pcount * (kPatchFloats / 4); t += 64) dst[t] = src[t];
+    }
+  }
+#endif
   if (U.lane == 0 && U.low) atomicAdd(&L.counters[1], U.low);
 }
 
@@ -304,12 +398,18 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
   const int per = P.S / L.ng, rem = P.S % L.ng;
   const int s_first = 1 + g * per + min(g, rem);
   const int cnt = per + (g < rem ? 1 : 0);
+#if SIFT_XREFINE
+  __shared__ __attribute__((aligned(16))) float xcap[4][kPatchUnitSlots * kPatchFloats];
+  float* const cap = xcap[threadIdx.x >> 6];
+#else
+  float* const cap = nullptr;
+#endif
   switch (cnt) {
-    case 1: x_scan<3, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
-    case 2: x_scan<4, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
-    case 3: x_scan<5, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
-    case 4: x_scan<6, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
-    default: x_scan<7, LOWL>(P, L, b, u, o, s_first, xw, y0, y1); break;
+    case 1: x_scan<3, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
+    case 2: x_scan<4, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
+    case 3: x_scan<5, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
+    case 4: x_scan<6, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
+    default: x_scan<7, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
   }
 }
 

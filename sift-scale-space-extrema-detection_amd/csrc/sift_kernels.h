@@ -105,7 +105,19 @@ struct ExtremaLaunch {
   float* patch;
   unsigned* wslot;
   int units_per_img;
+  // First refinement step in the scan (pre != nullptr, SIFT_XREFINE builds):
+  // the candidate's 19 values are captured into LDS instead of `patch`, and
+  // after its strip the unit takes the first step of background.js:480-664
+  // for each captured candidate (fp32 planes, the fast pass's error bounds),
+  // writing its outcome to pre[slot] (kPre* in .octave; a kept keypoint's
+  // record, or the position a move leads to with the candidate value in
+  // interp_value).  The fast refinement continues from there.
+  Keypoint* pre;
+  double min_blur, min_interpixel_distance;
 };
+// pre[slot].octave: the first step's outcome (kPreDefer: uncertain or
+// imprecise -- the fast refinement starts over from a gather).
+constexpr int kPreMoved = 0, kPreKeep = 1, kPreDiscard = 2, kPreSingular = 3, kPreDefer = 4;
 constexpr int kAmbWords = 8;     // counters slot: listed ambiguous words
 #ifndef SIFT_PATCH_SLOTS
 #define SIFT_PATCH_SLOTS 96
@@ -120,11 +132,15 @@ int extrema_units(const Pyramid& P);
 #ifndef SIFT_XPATCH
 #define SIFT_XPATCH 0
 #endif
+#ifndef SIFT_XREFINE
+#define SIFT_XREFINE 0
+#endif
+constexpr bool kXCapture = (SIFT_XPATCH != 0) || (SIFT_XREFINE != 0);  // the scan captures first-step patches (global / LDS)
 // Captured patch of a candidate at (s, y, x), d(k, a, c) = D_{s-1+k}(y-1+a, x-1+c):
 //   [0..8]   d(k, a, 1) at 3k + a (centre column, all three scales and rows) -- except d(2, 2, 1) at [16]
 //   [8..11]  d(1, 0, 0), d(1, 1, 0), d(1, 2, 0), d(0, 1, 0)   (left column)
 //   [12..15] d(1, 0, 2), d(1, 1, 2), d(1, 2, 2), d(0, 1, 2)   (right column)
-//   [16..19] d(2, 2, 1), d(2, 1, 0), d(2, 1, 2), unused
+//   [16..19] d(2, 2, 1), d(2, 1, 0), d(2, 1, 2), unused (LDS capture: the candidate's key - key of (s_first, 0, 0))
 // Five 16-byte pieces: the centre lane writes 2 + 1, each side lane 1 + 1.
 constexpr int kPatchFloats = 20;
 
@@ -203,6 +219,7 @@ struct RefineLaunch {
   int wide_exact;       // k_refine_exact: 256 threads per patch (latency) instead of one wave (throughput)
   const unsigned* cand_patch;  // per slot: captured first-step patch (ExtremaLaunch.patch), ~0u = gather; nullptr = none
   const float* patch;
+  const Keypoint* pre;  // != nullptr: cand_patch indexes the scan's first-step outcomes (ExtremaLaunch.pre) instead
 };
 
 // Processing order of the fast refinement (band_order): the slots of the
