@@ -59,6 +59,55 @@ struct XUnit {
   long long word0;     // index of (s_first, row 0, word 0) in L.bitmap (ambiguous word list)
 };
 
+// SIFT_XGLDS: the rows stream through a per-wave LDS ring of kXRing rows
+// (buffer_load_dword ... lds: no VGPR holds a row in flight), kXRing rows
+// ahead instead of the three the register window affords.
+#ifndef SIFT_XGLDS
+#define SIFT_XGLDS 0
+#endif
+#ifndef SIFT_XRING
+#define SIFT_XRING 5
+#endif
+constexpr int kXRing = SIFT_XRING;
+constexpr int kXRingFloats = kXRing * (kXMaxGroup + 2) * 64;  // one wave's ring
+
+template <int NP>
+struct XRing {
+  unsigned lds;     // LDS byte address of the wave's ring (wave-uniform)
+  unsigned vaddr;   // ... + lane * 4
+  int islot, cslot; // next slot to fill / to read
+  int next, last;   // next row to issue; rows past `last` re-read it
+};
+
+// Issues row ring.next (clamped) into slot islot: NP loads, one per plane.
+template <int NP>
+__device__ __forceinline__ void x_issue(const XUnit<NP>& U, XRing<NP>& R) {
+  const unsigned rofs = (unsigned)min(R.next, R.last) * (unsigned)U.w * 4u;
+  const unsigned base = R.lds + (unsigned)(R.islot * NP * 256);
+#pragma unroll
+  for (int q = 0; q < NP; ++q)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(U.rsrc, (__attribute__((address_space(3))) void*)(size_t)(base + q * 256), 4,
+                                             (int)U.xoff, (int)(rofs + (unsigned)q * U.plane_bytes), 0,
+                                             SIFT_XLOAD_AUX);
+  R.islot = R.islot + 1 == kXRing ? 0 : R.islot + 1;
+  ++R.next;
+}
+
+// The oldest row in flight (kXRing rows are: wait until kXRing - 1 remain),
+// read from its slot; its slot then takes the next row.
+template <int NP>
+__device__ __forceinline__ void x_take(const XUnit<NP>& U, XRing<NP>& R, float (&dst)[NP]) {
+  constexpr int N = NP * (kXRing - 1);  // loads younger than the row (stores in between only make this wait longer)
+  static_assert(N <= 63, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  const unsigned a = R.vaddr + (unsigned)(R.cslot * NP * 256);
+#pragma unroll
+  for (int q = 0; q < NP; ++q) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(dst[q]) : "v"(a), "i"(q * 256));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  R.cslot = R.cslot + 1 == kXRing ? 0 : R.cslot + 1;
+  x_issue(U, R);
+}
+
 template <int NP>
 __device__ __forceinline__ void x_load(const XUnit<NP>& U, float (&dst)[NP], int row) {
   // buffer loads: lane byte offset in a VGPR, row + plane offset in an SGPR
@@ -280,7 +329,7 @@ __device__ __forceinline__ void x_first_steps(const Pyramid& P, const ExtremaLau
 
 template <int NP, bool LOWL>
 __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L, int b, int u, int o, int s_first,
-                                       int xw, int y0, int y1, float* cap) {
+                                       int xw, int y0, int y1, float* cap, float* ring) {
   const Octave& oc = P.oct[o];
   XUnit<NP> U;
   U.plane = (long long)oc.h * oc.w;
@@ -321,6 +370,39 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   U.cap = cap;
   U.capa = (unsigned)(size_t)(__attribute__((address_space(3))) float*)cap;
   XWin<NP> Wn;
+#if SIFT_XGLDS
+  XRing<NP> R;
+  R.lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) float*)ring);
+  R.vaddr = R.lds + 4u * (unsigned)U.lane;
+  R.islot = R.cslot = 0;
+  R.next = y0 - 1;
+  R.last = y1 + 1;
+#pragma unroll
+  for (int k = 0; k < kXRing; ++k) x_issue(U, R);
+  {
+    float t[NP];
+    x_take(U, R, t);
+    x_derive<NP, 2>(Wn, t);
+    x_take(U, R, t);
+    x_derive<NP, 0>(Wn, t);
+  }
+  for (int y = y0; y <= y1; y += 3) {
+    float t[NP];
+    x_take(U, R, t);
+    x_derive<NP, 1>(Wn, t);
+    x_centre<NP, 2, 0, 1, LOWL>(Wn, U, L, y);
+    if (y + 1 > y1) break;
+    x_take(U, R, t);
+    x_derive<NP, 2>(Wn, t);
+    x_centre<NP, 0, 1, 2, LOWL>(Wn, U, L, y + 1);
+    if (y + 2 > y1) break;
+    x_take(U, R, t);
+    x_derive<NP, 0>(Wn, t);
+    x_centre<NP, 1, 2, 0, LOWL>(Wn, U, L, y + 2);
+  }
+  // the ring's last loads land in LDS: drained before the wave's LDS can be reallocated
+  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+#else
   {
     float r_m1[NP], r_0[NP];
     x_load(U, r_m1, y0 - 1);
@@ -346,6 +428,7 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
     x_load(U, Wn.raw[0], min(y + 6, y1 + 1));
     x_centre<NP, 1, 2, 0, LOWL>(Wn, U, L, y + 2);
   }
+#endif
 #if SIFT_XREFINE
   if (U.capture && U.pcount) {
     if constexpr (SIFT_XREFINE == 1) {
@@ -404,12 +487,18 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
 #else
   float* const cap = nullptr;
 #endif
+#if SIFT_XGLDS
+  __shared__ __attribute__((aligned(16))) float xring[4][kXRingFloats];
+  float* const ring = xring[threadIdx.x >> 6];
+#else
+  float* const ring = nullptr;
+#endif
   switch (cnt) {
-    case 1: x_scan<3, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
-    case 2: x_scan<4, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
-    case 3: x_scan<5, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
-    case 4: x_scan<6, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
-    default: x_scan<7, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap); break;
+    case 1: x_scan<3, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap, ring); break;
+    case 2: x_scan<4, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap, ring); break;
+    case 3: x_scan<5, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap, ring); break;
+    case 4: x_scan<6, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap, ring); break;
+    default: x_scan<7, LOWL>(P, L, b, u, o, s_first, xw, y0, y1, cap, ring); break;
   }
 }
 
