@@ -12,6 +12,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -85,6 +86,38 @@ void par_copy_rows(void* dst, size_t dpitch, const void* src, size_t spitch, siz
   }
   part(0, std::min(rows, per));
   for (auto& x : th) x.join();
+}
+
+// Host rows -> pinned staging -> device, pipelined: each of nt host threads
+// copies its share of the rows in ~2 MiB pieces and queues each piece's DMA on
+// `st` as soon as it is staged (disjoint ranges: their order does not matter;
+// the caller's later launches on `st` follow every piece).
+hipError_t h2d_rows_staged(void* dev, void* stage, const void* src, size_t spitch, size_t width, size_t rows, int nt,
+                           hipStream_t st) {
+  std::atomic<int> err{0};
+  auto part = [&](size_t r0, size_t r1) {
+    const size_t piece = std::max<size_t>(1, ((size_t)2 << 20) / width);
+    for (size_t a = r0; a < r1; a += piece) {
+      const size_t b = std::min(r1, a + piece);
+      for (size_t r = a; r < b; ++r) std::memcpy((char*)stage + r * width, (const char*)src + r * spitch, width);
+      if (hipMemcpyAsync((char*)dev + a * width, (const char*)stage + a * width, (b - a) * width,
+                         hipMemcpyHostToDevice, st) != hipSuccess)
+        err = 1;
+    }
+  };
+  if (nt <= 1 || rows * width < ((size_t)4 << 20)) {
+    part(0, rows);
+  } else {
+    std::vector<std::thread> th;
+    const size_t per = (rows + nt - 1) / nt;
+    for (int t = 1; t < nt; ++t) {
+      const size_t r0 = std::min(rows, t * per), r1 = std::min(rows, (t + 1) * per);
+      if (r0 < r1) th.emplace_back(part, r0, r1);
+    }
+    part(0, std::min(rows, per));
+    for (auto& x : th) x.join();
+  }
+  return err ? hipErrorUnknown : hipSuccess;
 }
 
 int host_threads() {
@@ -172,6 +205,7 @@ struct sift_ctx {
   DBuf keep, pos;                              // keypoint compaction
   DBuf band_cnt, band_first, band_start, perm;  // refinement band order
   DBuf status, kp_tmp, kp, uncertain;          // refinement
+  DBuf kp_soa;                                 // keypoint field arrays for a DMA into registered host arrays
   DBuf xseed, kp_key;                          // next-octave base, keypoint origins
   DBuf merge_tab;                              // sift_merge_keypoint_blocks_device tables
   DBuf counters, temp;
@@ -374,7 +408,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab,
                   &ctx->lowbitmap, &ctx->lowrowcount, &ctx->lowrowoff, &ctx->low_key, &ctx->low_val,
                   &ctx->late_key, &ctx->late_val, &ctx->band_cnt, &ctx->band_first, &ctx->band_start,
-                  &ctx->perm, &ctx->patch, &ctx->wslot, &ctx->cand_patch, &ctx->pre};
+                  &ctx->perm, &ctx->patch, &ctx->wslot, &ctx->cand_patch, &ctx->pre, &ctx->kp_soa};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -586,14 +620,30 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     // of it has completed.
     const size_t img_bytes = (size_t)W * H * nimg * sizeof(float);
     HIPCHK(ctx->img.ensure(img_bytes));
-    if (!ctx->ev_himg) HIPCHK(hipEventCreateWithFlags(&ctx->ev_himg, hipEventDisableTiming));
-    else HIPCHK(hipEventSynchronize(ctx->ev_himg));
-    HIPCHK(ctx->himg.ensure(img_bytes));
-    for (int b = 0; b < nimg; ++b)
-      par_copy_rows((float*)ctx->himg.p + (size_t)b * W * H, W * sizeof(float), img_host + (size_t)b * img_bstride,
-                    stride * sizeof(float), W * sizeof(float), H, host_threads());
-    HIPCHK(hipMemcpyAsync(ctx->img.p, ctx->himg.p, img_bytes, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipEventRecord(ctx->ev_himg, ctx->stream));
+    const bool dense = stride == (size_t)W && (nimg == 1 || img_bstride == (size_t)W * H);
+    if (dense && host_registered(img_host, img_bytes)) {
+      // page-locked caller memory (sift_host_register): one DMA straight from
+      // it -- every host-image entry point synchronises before it returns
+      HIPCHK(hipMemcpyAsync(ctx->img.p, img_host, img_bytes, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+      if (!ctx->ev_himg) HIPCHK(hipEventCreateWithFlags(&ctx->ev_himg, hipEventDisableTiming));
+      else HIPCHK(hipEventSynchronize(ctx->ev_himg));
+      HIPCHK(ctx->himg.ensure(img_bytes));
+#ifndef SIFT_H2D_PIPE
+#define SIFT_H2D_PIPE 1
+#endif
+      if (!SIFT_H2D_PIPE) {
+        for (int b = 0; b < nimg; ++b)
+          par_copy_rows((float*)ctx->himg.p + (size_t)b * W * H, W * sizeof(float), img_host + (size_t)b * img_bstride,
+                        stride * sizeof(float), W * sizeof(float), H, host_threads());
+        HIPCHK(hipMemcpyAsync(ctx->img.p, ctx->himg.p, img_bytes, hipMemcpyHostToDevice, ctx->stream));
+      } else
+      for (int b = 0; b < nimg; ++b)
+        HIPCHK(h2d_rows_staged(ctx->img.as<float>() + (size_t)b * W * H, (float*)ctx->himg.p + (size_t)b * W * H,
+                               img_host + (size_t)b * img_bstride, stride * sizeof(float), W * sizeof(float), H,
+                               host_threads(), ctx->stream));
+      HIPCHK(hipEventRecord(ctx->ev_himg, ctx->stream));
+    }
     P.img = ctx->img.as<float>();
     P.img_stride = W;
     P.img_bstride = nimg > 1 ? (long long)W * H : 0;
@@ -1481,6 +1531,18 @@ int sift_copy_keypoints_soa(sift_ctx* ctx, int32_t* ints, double* reals, size_t 
   const size_t n = ctx->n_kp;
   if (!n) return SIFT_OK;
   HIPCHK(hipSetDevice(ctx->device));
+  // Page-locked destinations (sift_host_register; the N-API result pool's
+  // recycled buffers): split on the device, one DMA into each array.
+  if (host_registered(ints, n * 4 * sizeof(int32_t)) && host_registered(reals, n * 4 * sizeof(double))) {
+    HIPCHK(ctx->kp_soa.ensure(n * sizeof(sift_keypoint)));
+    int32_t* di = ctx->kp_soa.as<int32_t>();
+    double* dr = reinterpret_cast<double*>(di + 4 * n);  // 16 n bytes in: 16-byte aligned
+    HIPCHK(launch_kp_soa(ctx->kp.as<Keypoint>(), (int)n, di, dr, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ints, di, n * 4 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(reals, dr, n * 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SIFT_OK;
+  }
   HIPCHK(ctx->hkp.ensure(n * sizeof(sift_keypoint)));
   HIPCHK(hipMemcpyAsync(ctx->hkp.p, ctx->kp.p, n * sizeof(sift_keypoint), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1852,8 +1914,11 @@ static int rgba_to_ctx_img(sift_ctx* ctx, const uint8_t* rgba, int W, int H, siz
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(ctx->rgba.ensure((size_t)W * H * 4));
   HIPCHK(ctx->img.ensure((size_t)W * H * sizeof(float)));
-  HIPCHK(hipMemcpy2DAsync(ctx->rgba.p, (size_t)W * 4, rgba, stride_bytes, (size_t)W * 4, H, hipMemcpyHostToDevice,
-                          ctx->stream));
+  if (stride_bytes == (size_t)W * 4 && host_registered(rgba, (size_t)W * H * 4))  // page-locked: one DMA
+    HIPCHK(hipMemcpyAsync(ctx->rgba.p, rgba, (size_t)W * H * 4, hipMemcpyHostToDevice, ctx->stream));
+  else
+    HIPCHK(hipMemcpy2DAsync(ctx->rgba.p, (size_t)W * 4, rgba, stride_bytes, (size_t)W * 4, H, hipMemcpyHostToDevice,
+                            ctx->stream));
   if (alpha) HIPCHK(ctx->alpha.ensure((size_t)W * H * sizeof(float)));
   HIPCHK(launch_rgba_to_gray(ctx->rgba.as<unsigned char>(), (size_t)W * 4, W, H, ctx->img.as<float>(),
                              alpha ? ctx->alpha.as<float>() : nullptr, ctx->stream));

@@ -69,7 +69,7 @@ struct XUnit {
 #define SIFT_XRING 5
 #endif
 constexpr int kXRing = SIFT_XRING;
-constexpr int kXRingFloats = kXRing * (kXMaxGroup + 2) * 64;  // one wave's ring
+[[maybe_unused]] constexpr int kXRingFloats = kXRing * (kXMaxGroup + 2) * 64;  // one wave's ring
 
 template <int NP>
 struct XRing {

@@ -332,6 +332,9 @@ constexpr long long kMergeChunk = 16384;
 hipError_t launch_merge_blocks(const Keypoint* in, const long long* seg, const long long* cstart, int nseg,
                                long long n_chunks, Keypoint* out, hipStream_t st);
 
+// Keypoint records -> field arrays (4 int32 + 4 doubles per keypoint, sift_copy_keypoints_soa's layout).
+hipError_t launch_kp_soa(const Keypoint* kp, int n, int32_t* ints, double* reals, hipStream_t st);
+
 // keys -> 4 int32 per keypoint: octave, scale, whole-image octave row (row0 applied), x.
 hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, int32_t* out, hipStream_t st);
 

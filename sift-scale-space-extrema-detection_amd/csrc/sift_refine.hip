@@ -384,6 +384,26 @@ hipError_t launch_decode_origins(const Pyramid& P, const unsigned* keys, int n, 
   return hipGetLastError();
 }
 
+// Keypoint records split into the field arrays callers take (ints: octave,
+// scale_level, local_x, local_y; reals: abs_sigma, abs_x, abs_y,
+// interp_value), so the host receives them by DMA with no reshuffle.
+__global__ __launch_bounds__(256) void k_kp_soa(const Keypoint* __restrict__ kp, int n, int4* __restrict__ ints,
+                                                double2* __restrict__ reals) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const Keypoint k = kp[i];
+  ints[i] = make_int4(k.octave, k.scale_level, k.local_x, k.local_y);
+  reals[2 * i] = make_double2(k.abs_sigma, k.abs_x);
+  reals[2 * i + 1] = make_double2(k.abs_y, k.interp_value);
+}
+
+hipError_t launch_kp_soa(const Keypoint* kp, int n, int32_t* ints, double* reals, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_kp_soa, dim3((n + 255) / 256), dim3(256), 0, st, kp, n, reinterpret_cast<int4*>(ints),
+                     reinterpret_cast<double2*>(reals));
+  return hipGetLastError();
+}
+
 // Deferred candidate values (EmitLaunch.deferred): the fp32 plane value of
 // every slot still holding the NaN marker.
 __global__ __launch_bounds__(256) void k_fill_values(const Pyramid P, const unsigned* __restrict__ keys,

@@ -11,14 +11,17 @@
  * Worker plays.
  */
 #define NAPI_VERSION 7  /* napi_detach_arraybuffer (releaseBuffer); Node >= 12.16 */
+#include <execinfo.h>
 #include <node_api.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "../../include/sift_hip.h"
 
@@ -1092,7 +1095,27 @@ static napi_value js_plane_image(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+/* SIFT_NAPI_SEGV_TRACE=1 (diagnostics): a fatal signal prints the native
+ * stack to stderr before the default action. */
+static void segv_trace(int sig) {
+  void *bt[64];
+  const int n = backtrace(bt, 64);
+  static const char msg[] = "sift_napi: fatal signal, native stack:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(bt, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 static napi_value init(napi_env env, napi_value exports) {
+  {
+    const char *t = getenv("SIFT_NAPI_SEGV_TRACE");
+    if (t && atoi(t)) {
+      signal(SIGSEGV, segv_trace);
+      signal(SIGBUS, segv_trace);
+      signal(SIGABRT, segv_trace);
+    }
+  }
   napi_property_descriptor props[] = {
       {"abiVersion", 0, js_abi_version, 0, 0, 0, napi_enumerable, 0},
       {"createContext", 0, js_create_context, 0, 0, 0, napi_enumerable, 0},
