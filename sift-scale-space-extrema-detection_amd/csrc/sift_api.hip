@@ -120,8 +120,15 @@ hipError_t h2d_rows_staged(void* dev, void* stage, const void* src, size_t spitc
   return err ? hipErrorUnknown : hipSuccess;
 }
 
+// Host threads of the library's own copies (image staging, keypoint split,
+// plane read-back): min(4, cores); SIFT_HOST_THREADS=n overrides it (a
+// process running several contexts at once, e.g. the N-API pool, may want 1).
 int host_threads() {
   static const int n = [] {
+    if (const char* e = std::getenv("SIFT_HOST_THREADS")) {
+      const int v = std::atoi(e);
+      if (v >= 1 && v <= 64) return v;
+    }
     const unsigned h = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(4u, h ? h : 1u));
   }();

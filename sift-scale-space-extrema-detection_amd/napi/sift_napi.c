@@ -346,12 +346,18 @@ typedef struct {
   int released;
 } pool_rec;
 
+/* Set by the environment's cleanup hook: the finalizers that follow (the
+ * environment's teardown runs every pending one) leave V8's accounting alone. */
+static volatile int g_env_closing = 0;
+
 static void pool_finalize(napi_env env, void *data, void *hint) {
   (void)data;
   pool_rec *r = (pool_rec *)hint;
   if (!r->released) {
-    int64_t adj;
-    napi_adjust_external_memory(env, -(int64_t)r->bytes, &adj);
+    if (!g_env_closing) {
+      int64_t adj;
+      napi_adjust_external_memory(env, -(int64_t)r->bytes, &adj);
+    }
     pool_give(r->p, r->bytes);
   }
   free(r);
@@ -1107,7 +1113,34 @@ static void segv_trace(int sig) {
   raise(sig);
 }
 
+static void on_env_cleanup(void *arg) {
+  (void)arg;
+  g_env_closing = 1;
+}
+
+/* At exit (before the HIP runtime's own teardown, whose handlers were
+ * registered earlier): the pooled buffers are unpinned while it still runs. */
+static void pool_atexit(void) {
+  pthread_mutex_lock(&g_pool_mu);
+  const int n = g_reg_n;
+  void *p[2 * POOL_SLOTS];
+  for (int i = 0; i < n; ++i) p[i] = g_reg[i].p;
+  g_reg_n = 0;
+  g_reg_bytes = 0;
+  pthread_mutex_unlock(&g_pool_mu);
+  for (int i = 0; i < n; ++i)
+    if (p[i]) (void)sift_host_unregister(p[i]);
+}
+
 static napi_value init(napi_env env, napi_value exports) {
+  napi_add_env_cleanup_hook(env, on_env_cleanup, NULL);
+  {
+    static int once = 0;
+    if (!once) {
+      once = 1;
+      atexit(pool_atexit);
+    }
+  }
   {
     const char *t = getenv("SIFT_NAPI_SEGV_TRACE");
     if (t && atoi(t)) {

@@ -20,7 +20,12 @@ const opts = { number_of_octaves: O, scales_per_octave: S, min_blur_level: 0.8, 
 const mpix = W * H / 1e6;
 async function main() {
 const med = (a) => { const b = [...a].sort((x, y) => x - y); return b[b.length >> 1]; };
-const out = { width: W, height: H, octaves: O, scales: S, reps, node: process.version };
+const out = { width: W, height: H, octaves: O, scales: S, reps, node: process.version, node_flags: process.execArgv };
+// Every timed section starts from a collected heap (node --expose-gc): a 4K
+// result is 445 K keypoint objects (~40 MB of JS heap), and results a previous
+// section still held would turn the next one's collections into full
+// mark-sweeps near the heap limit.
+const gc = () => { if (global.gc) { global.gc(); global.gc(); } };
 
 // 1. detect (synchronous; the device work is serialised in the call)
 let kp = sift.detect(image, opts);  // warm-up (allocations, code objects)
@@ -44,17 +49,23 @@ out.detect.host_other_ms = out.detect.wall_ms - (out.detect.h2d_ms + out.detect.
   + out.detect.refine_ms + out.detect.d2h_ms);
 
 // 2. detectAsync: one at a time, then `reps` images queued at once
+kp = null;
+gc();
 const awall = [];
 for (let i = 0; i < reps; i++) {
   const t0 = performance.now();
   kp = await sift.detectAsync(image, opts);
   awall.push(performance.now() - t0);
 }
+const nkA = kp.length;
+kp = null;
+gc();
 const tq = performance.now();
-const all = await Promise.all(Array.from({ length: reps }, () => sift.detectAsync(image, opts)));
+let all = await Promise.all(Array.from({ length: reps }, () => sift.detectAsync(image, opts)));
 const qms = performance.now() - tq;
+all = null;
 out.detectAsync = {
-  keypoints: all[0].length, wall_ms: med(awall), mpix_per_s: mpix / (med(awall) / 1e3),
+  keypoints: nkA, wall_ms: med(awall), mpix_per_s: mpix / (med(awall) / 1e3),
   queued_images: reps, queued_total_ms: qms, queued_mpix_per_s: reps * mpix / (qms / 1e3),
   d2h_ms: sift.lastTimings().d2hMs,
   what: 'await sift.detectAsync(image): the same call on the libuv pool (keypoint copy on the worker thread); '
@@ -82,11 +93,14 @@ out.detectAsync = {
     ['detectAsync_objects_queued', { ...opts, inflight: 3 }],
     ['detectAsync_typed_queued_inflight1', { ...topts, inflight: 1 }]]) {
     await Promise.all(Array.from({ length: 3 }, () => sift.detectAsync(image, o)));  // pool warm-up
+    gc();
     const t0 = performance.now();
-    const rs = await Promise.all(Array.from({ length: nq }, () => sift.detectAsync(image, o)));
+    let rs = await Promise.all(Array.from({ length: nq }, () => sift.detectAsync(image, o)));
     const ms = performance.now() - t0;
+    const nk0 = rs[0].count !== undefined ? rs[0].count : rs[0].length;
+    rs = null;
     out[name] = {
-      keypoints: rs[0].count !== undefined ? rs[0].count : rs[0].length, images: nq, total_ms: ms,
+      keypoints: nk0, images: nq, total_ms: ms,
       ms_per_image: ms / nq, mpix_per_s: nq * mpix / (ms / 1e3),
       what: `Promise.all over ${nq} detectAsync(image, ${JSON.stringify({ format: o.format || 'objects', inflight: o.inflight })})`,
     };
@@ -100,6 +114,7 @@ out.detectAsync = {
 {
   const nq = Math.max(3 * reps, 12), depth = 3;
   for (let i = 0; i < 3; i++) await sift.detectAsync(image, opts);
+  gc();
   const t0 = performance.now();
   const q = [];
   let nkp = 0;

@@ -18,13 +18,18 @@ ap.add_argument("--height", type=int, default=2160)
 ap.add_argument("--octaves", type=int, default=4)
 ap.add_argument("--scales", type=int, default=5)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--heap-mb", type=int, default=8192, help="node --max-old-space-size")
 ap.add_argument("--out", required=True)
 a = ap.parse_args()
 img = blob_image(a.width, a.height, seed=42)
 f32 = a.out + ".f32"
 img.astype("<f4").tofile(f32)
 try:
-    sys.exit(subprocess.call(["node", os.path.join(R, "tools", "js_bench", "bench_js.mjs"), f32, str(a.width),
+    # --expose-gc: each timed section starts from a collected heap; a larger
+    # old space: Promise.all over 30 4K results holds ~13 M keypoint objects
+    # (~1.3 GB), at which the default limit (~1.7 GB here) aborts the process
+    sys.exit(subprocess.call(["node", "--expose-gc", "--max-old-space-size=%d" % a.heap_mb,
+                              os.path.join(R, "tools", "js_bench", "bench_js.mjs"), f32, str(a.width),
                               str(a.height), str(a.octaves), str(a.scales), str(a.reps), a.out]))
 finally:
     os.remove(f32)
