@@ -60,11 +60,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     const float* __restrict__ D = P.dog + im * P.dog_bstride + oc.dog_off;
     // the first step's patch as captured by the scan (kPatchFloats layout), if any
     const unsigned pidx = L.cand_patch ? L.cand_patch[i] : ~0u;
-    const bool patched = pidx != ~0u && L.patch;
+    // (with SIFT_XREFINE=1 cand_patch indexes L.pre instead: no patch buffer)
+    const bool patched = pidx != ~0u && (SIFT_XREFINE != 1 || L.patch);
     const float* __restrict__ pp = L.patch + (size_t)(patched ? pidx : 0u) * kPatchFloats;
     double value = L.cand_val[i];
     int status = kRefDiscard;
     int it0 = 0;
+#if SIFT_XREFINE == 1
     // The scan's first step (L.pre): taken on the fp32 plane value, so only
     // for candidates whose value is still deferred (an exact re-decision
     // writes the fp64 value, and the chain starts over from it).
@@ -89,6 +91,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         it0 = 1;
       }
     }
+#endif
     if (value != value)  // deferred: the fp32 plane value
       value = patched ? (double)pp[4] : (double)D[s * plane + (long long)m * w + n];
     const double dval = EXACT ? 0.0 : fabs(value) * 0x1p-24;
