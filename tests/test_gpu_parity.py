@@ -230,6 +230,46 @@ def test_keypoint_field_arrays_equal_records(gpu_ctx):
     assert gpu_ctx.keypoints().tobytes() == kp.tobytes()
 
 
+def test_page_locked_image_and_field_arrays(gpu_ctx):
+    """Page-locked host memory (sift_host_register): the image goes up by one
+    DMA straight from it, and sift_copy_keypoints_soa splits the records on
+    the device and DMAs the fields straight into page-locked destinations --
+    the same keypoints and fields as the staged paths (a pageable image, and
+    destinations through the pinned staging)."""
+    import ctypes
+    import mmap
+    W, H = 1024, 600
+    img = blob_image(W, H, seed=31)
+    p = sift_amd.make_params(4, 3)
+    gpu_ctx.detect(np.ascontiguousarray(img), p)
+    ref = gpu_ctx.keypoints()
+    ints0, reals0 = gpu_ctx.keypoints_soa()
+    n = ref.shape[0]
+    assert n > 100
+    L = gpu_ctx._L
+    bufs = [mmap.mmap(-1, W * H * 4), mmap.mmap(-1, n * 16), mmap.mmap(-1, n * 32)]  # page-aligned
+    a = np.frombuffer(bufs[0], dtype=np.float32).reshape(H, W)
+    a[:] = img
+    ints = np.frombuffer(bufs[1], dtype=np.int32).reshape(n, 4)
+    reals = np.frombuffer(bufs[2], dtype=np.float64).reshape(n, 4)
+    ptrs = [a.ctypes.data, ints.ctypes.data, reals.ctypes.data]
+    for q, b in zip(ptrs, bufs):
+        assert L.sift_host_register(ctypes.c_void_p(q), len(b)) == 0
+    try:
+        gpu_ctx.detect(a, p)
+        assert gpu_ctx.keypoints().tobytes() == ref.tobytes()
+        got = ctypes.c_size_t()
+        assert L.sift_copy_keypoints_soa(gpu_ctx._h, ctypes.c_void_p(ptrs[1]), ctypes.c_void_p(ptrs[2]), n,
+                                         ctypes.byref(got)) == 0
+        assert got.value == n
+        np.testing.assert_array_equal(ints, ints0)
+        np.testing.assert_array_equal(reals, reals0)
+    finally:
+        for q in ptrs:
+            L.sift_host_unregister(ctypes.c_void_p(q))
+        del a, ints, reals
+
+
 def test_foreign_scale_space_dog(gpu_ctx):
     """computeDifferenceOfGaussians on a caller scale space: D = L[s-1]-L[s]."""
     img = blob_image(96, 80, seed=22)
