@@ -201,12 +201,14 @@ def main():
                          "image k+1 runs).  Default: 2 for single images of >= 4 Mpix (4K: 2 > 3 by 1.5-2 %%, "
                          "profiles/r4am_inflight_ab.txt), 3 for smaller ones (1080p: +15 %%, "
                          "profiles/r5h_cfg2_inflight.txt) and for batched launches (cfg 4: 3 > 2 by 3 %%, DESIGN 8a)")
-    ap.add_argument("--overlap", default="octave0",
+    ap.add_argument("--overlap", default=None,
                     choices=["none", "octave0", "gaussian", "refinement", "full", "phased"],
                     help="how consecutive images overlap on the GPU: none = contexts share one stream; "
                          "octave0 / gaussian / refinement = own streams, image k+1 starts once image k has "
                          "passed that point (sift_order_after: software pipelining); full = own streams, "
-                         "no ordering.  Per-kernel durations (roofline.achieved) include any overlap")
+                         "no ordering.  Default: full for single images of 4 Mpix and more (3 in flight), "
+                         "octave0 otherwise (profiles/r5w_schedule_ab.txt).  Per-kernel durations "
+                         "(roofline.achieved) include any overlap")
     ap.add_argument("--shard-image", action="store_true",
                     help="BASELINE cfg 5: ONE image per step split over all ranks in row bands (sift_amd.shard."
                          "detect_sharded_device: band octaves, all-gathered next-octave base, tail octaves one per "
@@ -259,6 +261,11 @@ def main():
     d_img = torch.from_numpy(img).to("cuda:%d" % dev)
     Bt = max(1, args.batch)
     batched = Bt > 1 and args.batch_mode == "launch"
+    if args.overlap is None:
+        # single large images: three contexts with no ordering between them (4K: 7.18 against 7.00
+        # Gpix/s for octave0 with two, and steadier, over 5 paired runs); batches and small images
+        # keep octave0 (profiles/r5w_schedule_ab.txt)
+        args.overlap = "full" if args.batch == 1 and W * H >= 4000000 else "octave0"
     if batched and args.overlap == "phased":
         print("bench.py: --overlap phased does not apply to batched launches", file=sys.stderr)
         return 2
@@ -267,11 +274,11 @@ def main():
         d_imgs = torch.from_numpy(np.stack([img] + [blob_image(W, H, seed=1000 + 64 * rank + i)
                                                    for i in range(1, Bt)])).to("cuda:%d" % dev)
     torch.cuda.synchronize(dev)
-    # in flight: 2 for single 4K images (2 > 3 by 1.5-2 %, profiles/r4am_inflight_ab.txt), 3 for batched
-    # launches and for single images up to ~1080p (1080p: 5.20 / 5.96 / 5.10 Gpix/s at 2 / 3 / 4,
-    # profiles/r5h_cfg2_inflight.txt: a small image leaves the chip room for a third)
+    # in flight: 3 (single 4K images with overlap full, profiles/r5w_schedule_ab.txt; batched launches;
+    # single images up to ~1080p: 5.20 / 5.96 / 5.10 Gpix/s at 2 / 3 / 4, profiles/r5h_cfg2_inflight.txt);
+    # 2 for large single images under an ordered schedule (octave0: 2 > 3 by 1.5-2 %, r4am_inflight_ab.txt)
     nin = max(1, args.inflight if args.inflight is not None else
-              (3 if args.batch > 1 or W * H < 4000000 else 2))
+              (3 if args.batch > 1 or W * H < 4000000 or args.overlap == "full" else 2))
     ctxs = [sift_amd.Context(dev)]
     own = args.overlap != "none"
     after = {"octave0": sift_amd.AFTER_OCTAVE0, "gaussian": sift_amd.AFTER_GAUSSIAN,
