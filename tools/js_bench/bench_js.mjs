@@ -28,18 +28,28 @@ const out = { width: W, height: H, octaves: O, scales: S, reps, node: process.ve
 const gc = () => { if (global.gc) { global.gc(); global.gc(); } };
 
 // 1. detect (synchronous; the device work is serialised in the call)
+gc();
 let kp = sift.detect(image, opts);  // warm-up (allocations, code objects)
 sift.detect(image, opts);
 const wall = [], tm = [];
-for (let i = 0; i < reps; i++) {
+// (no collection between the warm-up and the timed calls: forced right after
+// two calls, it left the keypoint-object loop unoptimised for the whole
+// section on the box -- 334 instead of ~15 ms per 4K call)
+const nsync = Math.max(3 * reps, 12);  // as many images as the queued rows below
+const tsync = performance.now();
+for (let i = 0; i < nsync; i++) {
   const t0 = performance.now();
   kp = sift.detect(image, opts);
   wall.push(performance.now() - t0);
   tm.push(sift.lastTimings());
 }
+const syncMean = (performance.now() - tsync) / nsync;
 const pick = (k) => med(tm.map((t) => t[k]));
 out.detect = {
   keypoints: kp.length, wall_ms: med(wall), mpix_per_s: mpix / (med(wall) / 1e3),
+  // the queued / streamed rows below are totals over their images (collections included): compare them
+  // with this mean, not with the median (which leaves out the calls a collection lands in)
+  mean_ms: syncMean, mean_mpix_per_s: mpix / (syncMean / 1e3),
   h2d_ms: pick('h2dMs'), gauss_dog_ms: pick('gaussDogMs'), extrema_ms: pick('extremaMs'), refine_ms: pick('refineMs'),
   d2h_ms: pick('d2hMs'),
   what: 'sift.detect(ImageData-shaped Float32 host image) -> keypoint objects; wall = host clock around the call '
