@@ -32,6 +32,7 @@ import re
 import sys
 import time
 
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sift-scale-space-extrema-detection_amd"))
 
@@ -206,8 +207,7 @@ def main():
                     help="how consecutive images overlap on the GPU: none = contexts share one stream; "
                          "octave0 / gaussian / refinement = own streams, image k+1 starts once image k has "
                          "passed that point (sift_order_after: software pipelining); full = own streams, "
-                         "no ordering.  Default: full for single images of 4 Mpix and more (3 in flight), "
-                         "octave0 otherwise (profiles/r5w_schedule_ab.txt).  Per-kernel durations "
+                         "no ordering.  Default: full (profiles/r5w_schedule_ab.txt).  Per-kernel durations "
                          "(roofline.achieved) include any overlap")
     ap.add_argument("--shard-image", action="store_true",
                     help="BASELINE cfg 5: ONE image per step split over all ranks in row bands (sift_amd.shard."
@@ -262,10 +262,10 @@ def main():
     Bt = max(1, args.batch)
     batched = Bt > 1 and args.batch_mode == "launch"
     if args.overlap is None:
-        # single large images: three contexts with no ordering between them (4K: 7.18 against 7.00
-        # Gpix/s for octave0 with two, and steadier, over 5 paired runs); batches and small images
-        # keep octave0 (profiles/r5w_schedule_ab.txt)
-        args.overlap = "full" if args.batch == 1 and W * H >= 4000000 else "octave0"
+        # contexts with no ordering between them (4K single images: 7.18 against 7.00 Gpix/s for
+        # octave0 with two, and steadier; 1080p singles and batches of 8 with four contexts: +7 / +3 %
+        # over octave0 with three; profiles/r5w_schedule_ab.txt)
+        args.overlap = "full"
     if batched and args.overlap == "phased":
         print("bench.py: --overlap phased does not apply to batched launches", file=sys.stderr)
         return 2
@@ -274,11 +274,20 @@ def main():
         d_imgs = torch.from_numpy(np.stack([img] + [blob_image(W, H, seed=1000 + 64 * rank + i)
                                                    for i in range(1, Bt)])).to("cuda:%d" % dev)
     torch.cuda.synchronize(dev)
-    # in flight: 3 (single 4K images with overlap full, profiles/r5w_schedule_ab.txt; batched launches;
-    # single images up to ~1080p: 5.20 / 5.96 / 5.10 Gpix/s at 2 / 3 / 4, profiles/r5h_cfg2_inflight.txt);
-    # 2 for large single images under an ordered schedule (octave0: 2 > 3 by 1.5-2 %, r4am_inflight_ab.txt)
-    nin = max(1, args.inflight if args.inflight is not None else
-              (3 if args.batch > 1 or W * H < 4000000 or args.overlap == "full" else 2))
+    # in flight (overlap full; profiles/r5w_schedule_ab.txt): 3 for single images of 4 Mpix and more
+    # (4K: 3 > 4 by 1-2 %; 8K: equal); for smaller single images and batched launches 4 when the process
+    # runs with GPU_MAX_HW_QUEUES >= 8 (1080p: 6.31-6.46 against 6.10 Gpix/s with 3; 1080p x 8: 7.35-7.45
+    # against 7.14-7.18) -- with the runtime's default 4 queues a fourth context shares a queue with
+    # another and they run in turn (1080p: 5.26-5.30), so 3 there.  The variable is read when the HIP
+    # runtime loads, before this script runs: it has to come from the caller's environment.  Under an
+    # ordered schedule 2 for large single images (octave0: 2 > 3 by 1.5-2 %, r4am_inflight_ab.txt).
+    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    if args.inflight is not None:
+        nin = max(1, args.inflight)
+    elif args.overlap == "full":
+        nin = 3 if (args.batch == 1 and W * H >= 4000000) or hwq < 8 else 4
+    else:
+        nin = 3 if args.batch > 1 or W * H < 4000000 else 2
     ctxs = [sift_amd.Context(dev)]
     own = args.overlap != "none"
     after = {"octave0": sift_amd.AFTER_OCTAVE0, "gaussian": sift_amd.AFTER_GAUSSIAN,
