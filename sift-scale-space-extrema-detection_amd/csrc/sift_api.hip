@@ -121,14 +121,12 @@ hipError_t h2d_rows_staged(void* dev, void* stage, const void* src, size_t spitc
 }
 
 // Host threads of the library's own copies (image staging, keypoint split,
-// plane read-back): min(4, cores); SIFT_HOST_THREADS=n overrides it (a
-// process running several contexts at once, e.g. the N-API pool, may want 1).
+// plane read-back): min(4, cores); SIFT_HOST_THREADS=n in experiments builds
+// (1, 2 and 4 measured under the N-API pool: 4 is best).
 int host_threads() {
   static const int n = [] {
-    if (const char* e = std::getenv("SIFT_HOST_THREADS")) {
-      const int v = std::atoi(e);
-      if (v >= 1 && v <= 64) return v;
-    }
+    const int v = exp_knob("SIFT_HOST_THREADS", 0);
+    if (v >= 1 && v <= 64) return v;
     const unsigned h = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(4u, h ? h : 1u));
   }();
