@@ -69,4 +69,6 @@ async function main() {
   out.pinCapMB = Number(process.env.SIFT_NAPI_PIN_MB || 0);
   fs.writeFileSync(outPath, JSON.stringify(out));
 }
-main().catch((e) => { console.error(e); process.exit(1); });
+// process.exit: Node 12's teardown may run queued N-API finalizers on a dead
+// isolate (profiles/r5ag_node12_exit_finalizer.txt)
+main().then(() => process.exit(0), (e) => { console.error(e); process.exit(1); });
