@@ -433,7 +433,9 @@ export function detectBatch(images, { number_of_octaves = 5, scales_per_octave =
 }
 
 // Asynchronous detections run on a pool of `inflight` contexts per device
-// (default 3; each has its own HIP stream and pyramid), so up to that many
+// (default 4 below 4 Mpix, 3 from there up -- the pool sizes measured best on
+// MI355X with Node's 4 hardware queues, profiles/r5ah_js_inflight_probe.txt;
+// each context has its own HIP stream and pyramid), so up to that many
 // images are on the GPU at once and one image's host work (H2D of the
 // input, keypoint copy, result conversion) overlaps the others' device
 // work.  Jobs beyond the pool wait in FIFO order.  The pool's first context
@@ -456,9 +458,15 @@ function releaseSlot(pool, slot) {
   }
 }
 
+function defaultInflight(img) {
+  const px = img && Number.isFinite(img.width) && Number.isFinite(img.height) ? img.width * img.height : 0;
+  return px > 0 && px < 4e6 ? 4 : 3;
+}
+
 export function detectAsync(input_image, opts = {}) {
   const { number_of_octaves = 5, scales_per_octave = 3, min_blur_level = 0.8, assumed_blur = 0.5,
-    min_interpixel_distance = 0.5, device = 0, inflight = 3, format } = opts;
+    min_interpixel_distance = 0.5, device = 0, format } = opts;
+  const inflight = opts.inflight !== undefined ? opts.inflight : defaultInflight(input_image);
   const st = deviceState(device);
   const pool = asyncPool(st, inflight);
   const limit = Math.max(1, inflight | 0);

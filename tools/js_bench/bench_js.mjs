@@ -99,10 +99,13 @@ out.detectAsync = {
     what: "sift.detect(image, {format: 'typed'}) -> {count, ints, doubles}: the same records without JS objects",
   };
   const nq = Math.max(3 * reps, 12);
-  for (const [name, o] of [['detectAsync_typed_queued', { ...topts, inflight: 3 }],
-    ['detectAsync_objects_queued', { ...opts, inflight: 3 }],
+  for (const [name, o] of [['detectAsync_typed_queued', { ...topts }],
+    ['detectAsync_objects_queued', { ...opts }],
     ['detectAsync_typed_queued_inflight1', { ...topts, inflight: 1 }]]) {
-    await Promise.all(Array.from({ length: 3 }, () => sift.detectAsync(image, o)));  // pool warm-up
+    // warm-up: one untimed loop of the same shape (grows the context pool and
+    // the result-buffer pool to their steady-state sizes)
+    await Promise.all(Array.from({ length: nq }, () => sift.detectAsync(image, o)));
+    gc();
     gc();
     const t0 = performance.now();
     let rs = await Promise.all(Array.from({ length: nq }, () => sift.detectAsync(image, o)));
@@ -112,7 +115,7 @@ out.detectAsync = {
     out[name] = {
       keypoints: nk0, images: nq, total_ms: ms,
       ms_per_image: ms / nq, mpix_per_s: nq * mpix / (ms / 1e3),
-      what: `Promise.all over ${nq} detectAsync(image, ${JSON.stringify({ format: o.format || 'objects', inflight: o.inflight })})`,
+      what: `Promise.all over ${nq} detectAsync(image, ${JSON.stringify({ format: o.format || 'objects', inflight: o.inflight === undefined ? 'default' : o.inflight })})`,
     };
   }
 }
