@@ -1739,8 +1739,17 @@ __global__ __launch_bounds__(256) void k_seed_vert(const Pyramid P, int o, const
   const double* __restrict__ wt = P.wts + oc.wofs[P.S];
   const double* __restrict__ col = base + x;
   const long long w = oc.w;
+  // eight loads in flight ahead of their fma steps (the chain's order is kept)
   double acc = 0.0;
-  for (int j = 0; j <= 2 * r; ++j) acc = __builtin_fma(wt[j], col[clampi(2 * yp + j - r, 0, h - 1) * w], acc);
+  int j = 0;
+  for (; j + 8 <= 2 * r + 1; j += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = col[clampi(2 * yp + j + k - r, 0, h - 1) * w];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = __builtin_fma(wt[j + k], v[k], acc);
+  }
+  for (; j <= 2 * r; ++j) acc = __builtin_fma(wt[j], col[clampi(2 * yp + j - r, 0, h - 1) * w], acc);
   vrow[(long long)yp * w + x] = acc;
 }
 
@@ -1754,7 +1763,15 @@ __global__ __launch_bounds__(256) void k_seed_horz(const Pyramid P, int o, const
   const double* __restrict__ wt = P.wts + oc.wofs[P.S];
   const double* __restrict__ row = vrow + (long long)yp * w;
   double acc = 0.0;
-  for (int i = 0; i <= 2 * r; ++i) acc = __builtin_fma(wt[i], row[clampi(2 * xp + i - r, 0, w - 1)], acc);
+  int i = 0;
+  for (; i + 8 <= 2 * r + 1; i += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = row[clampi(2 * xp + i + k - r, 0, w - 1)];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc = __builtin_fma(wt[i + k], v[k], acc);
+  }
+  for (; i <= 2 * r; ++i) acc = __builtin_fma(wt[i], row[clampi(2 * xp + i - r, 0, w - 1)], acc);
   next[(long long)yp * nw + xp] = acc;
 }
 
