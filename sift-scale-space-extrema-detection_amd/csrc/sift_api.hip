@@ -208,6 +208,7 @@ struct sift_ctx {
   DBuf lowbitmap, lowrowcount, lowrowoff;      // low-contrast list (SIFT_F_LOW_CONTRAST_LIST)
   DBuf low_key, low_val, late_key, late_val;
   DBuf keep, pos;                              // keypoint compaction
+  DBuf keep_tile;                              // ... its per-tile counts (launch_keep_compact)
   DBuf band_cnt, band_first, band_start, perm;  // refinement band order
   DBuf status, kp_tmp, kp, uncertain;          // refinement
   DBuf kp_soa;                                 // keypoint field arrays for a DMA into registered host arrays
@@ -413,7 +414,7 @@ int sift_ctx_destroy(sift_ctx* ctx) {
                   &ctx->temp, &ctx->rgba, &ctx->alpha, &ctx->display, &ctx->mm_parts, &ctx->merge_tab,
                   &ctx->lowbitmap, &ctx->lowrowcount, &ctx->lowrowoff, &ctx->low_key, &ctx->low_val,
                   &ctx->late_key, &ctx->late_val, &ctx->band_cnt, &ctx->band_first, &ctx->band_start,
-                  &ctx->perm, &ctx->patch, &ctx->wslot, &ctx->cand_patch, &ctx->pre, &ctx->kp_soa};
+                  &ctx->perm, &ctx->patch, &ctx->wslot, &ctx->cand_patch, &ctx->pre, &ctx->kp_soa, &ctx->keep_tile};
   for (DBuf* b : bufs) b->release();
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1304,6 +1305,12 @@ static int refine_enqueue(sift_ctx* ctx) {
     // Uncertain decisions exist only with fp32-rounded native planes.
     R.wide_exact = ctx->o_first > 0;  // a tail piece (sift_detect_from_seed*): latency over throughput
     if (ctx->dog_source == kNative) HIPCHK(launch_refine_exact(P, R, ctx->stream));
+#if SIFT_KEEP_SCAN
+    HIPCHK(ctx->keep_tile.ensure(keep_tiles(cap) * sizeof(unsigned)));
+    HIPCHK(launch_keep_compact(P, R.status, R.cand_key, ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(),
+                               ctx->keep_tile.as<unsigned>(), R.n, cap, ctx->own_lo, ctx->own_hi, cnt + kBlk, R.kp,
+                               ctx->kp.as<Keypoint>(), ctx->stream));
+#else
     HIPCHK(launch_status_to_keep(P, R.status, R.cand_key, ctx->keep.as<unsigned>(), R.n, cap, ctx->own_lo,
                                  ctx->own_hi, cnt + kBlk, ctx->stream));
     size_t tb = 0;
@@ -1315,6 +1322,7 @@ static int refine_enqueue(sift_ctx* ctx) {
                                             ctx->stream));
     HIPCHK(launch_scatter_keypoints(ctx->keep.as<unsigned>(), ctx->pos.as<unsigned>(), R.kp, R.n, cap,
                                     ctx->kp.as<Keypoint>(), ctx->stream));
+#endif
     HIPCHK(launch_count_keypoints(P, ctx->pos.as<unsigned>(), ctx->keep.as<unsigned>(), R.cand_key, R.n, cap,
                                   cnt + kCntKp, cnt + kBlk, ctx->stream));
     if (ctx->p.flags & SIFT_F_KEYPOINT_ORIGINS) {

@@ -316,6 +316,19 @@ hipError_t launch_status_to_keep(const Pyramid& P, const int* status, const unsi
                                  const unsigned* n, int cap, int own_lo, int own_hi, unsigned* blk, hipStream_t st);
 hipError_t launch_scatter_keys(const unsigned* keep, const unsigned* pos, const unsigned* key, const unsigned* n,
                                int cap, unsigned* out, hipStream_t st);
+// launch_status_to_keep + an exclusive scan of keep into pos +
+// launch_scatter_keypoints, with the work bounded by *n instead of cap: keep
+// and pos are written for the slots of the tiles up to slot min(*n, cap)
+// (what launch_count_keypoints and launch_scatter_keys read); tile holds
+// keep_tiles(cap) words of scratch.
+#ifndef SIFT_KEEP_SCAN
+#define SIFT_KEEP_SCAN 1  // 0: capacity-sized device scan (the round-4 compaction; A/B builds)
+#endif
+constexpr int kKeepTile = 2048;
+inline size_t keep_tiles(int cap) { return cap > 0 ? (size_t)(cap + kKeepTile - 1) / kKeepTile : 0; }
+hipError_t launch_keep_compact(const Pyramid& P, const int* status, const unsigned* key, unsigned* keep,
+                               unsigned* pos, unsigned* tile, const unsigned* n, int cap, int own_lo, int own_hi,
+                               unsigned* blk, const Keypoint* kp, Keypoint* out, hipStream_t st);
 // out = pos[n-1] + keep[n-1] (0 if n == 0): the number of keypoints; blk[b] =
 // kept keypoints of block b, from the block starts and the exclusive scan pos
 // (a histogram over the slots when the list was not in key order).

@@ -260,14 +260,10 @@ __device__ __forceinline__ int key_block(const Pyramid& P, unsigned key) {
   return (im * P.O + o) * P.S + (s - 1);
 }
 
-__global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const int* __restrict__ status,
-                                                        const unsigned* __restrict__ key,
-                                                        unsigned* __restrict__ keep, const unsigned* __restrict__ n,
-                                                        int cap, int own_lo, int own_hi,
-                                                        unsigned* __restrict__ blk) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= cap) return;
-  const int m = (int)min(*n, (unsigned)cap);
+// Keep flag of slot i < cap of a list of m candidates (and the block starts it opens).
+__device__ __forceinline__ bool keep_slot(const Pyramid& P, const int* __restrict__ status,
+                                          const unsigned* __restrict__ key, int i, int m, int own_lo, int own_hi,
+                                          unsigned* __restrict__ blk) {
   bool k = false;
   if (i < m) {
     int im, o, s, y, x;
@@ -288,7 +284,115 @@ __global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const i
     if (i == m - 1)
       for (int q = max(b, bp) + 1; q <= nb; ++q) blk[kBlkStart + q] = (unsigned)m;
   }
-  keep[i] = k ? 1u : 0u;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void k_status_to_keep(const Pyramid P, const int* __restrict__ status,
+                                                        const unsigned* __restrict__ key,
+                                                        unsigned* __restrict__ keep, const unsigned* __restrict__ n,
+                                                        int cap, int own_lo, int own_hi,
+                                                        unsigned* __restrict__ blk) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= cap) return;
+  const int m = (int)min(*n, (unsigned)cap);
+  keep[i] = keep_slot(P, status, key, i, m, own_lo, own_hi, blk) ? 1u : 0u;
+}
+
+// ---------------------------------------------------------------------------
+// Compaction bounded by the device count (launch_keep_compact): the slots are
+// cut into tiles of kKeepTile; only the tiles up to the one holding slot m
+// (= min(*n, cap)) do any work, where a capacity-sized device scan reads and
+// writes every slot (4.6 M at 8K: 26 us for the scan alone, whatever m is).
+// k_keep_flags: keep flags and block starts (keep_slot), one count per tile;
+// k_keep_scan: exclusive scan of the tile counts (one workgroup);
+// k_keep_scatter: pos[i] (in-tile prefix by wave ballots) and the kept
+// keypoints' copies.  pos[i] is written for every slot of the tiles <= m's,
+// so pos[m] (m < cap) is the total, as launch_count_keypoints reads it.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned block_sum256(unsigned c, unsigned* ws) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if (lane == 0) ws[w] = c;
+  __syncthreads();
+  return ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(256) void k_keep_flags(const Pyramid P, const int* __restrict__ status,
+                                                    const unsigned* __restrict__ key, unsigned* __restrict__ keep,
+                                                    const unsigned* __restrict__ n, int cap, int own_lo, int own_hi,
+                                                    unsigned* __restrict__ blk, unsigned* __restrict__ tile) {
+  const int m = (int)min(*n, (unsigned)cap);
+  const int t0 = blockIdx.x * kKeepTile;
+  if (t0 > m) return;  // block-uniform: tiles past the count are never read
+  __shared__ unsigned ws[4];
+  unsigned c = 0;
+#pragma unroll
+  for (int k = 0; k < kKeepTile / 256; ++k) {
+    const int i = t0 + k * 256 + (int)threadIdx.x;
+    if (i < cap) {
+      const bool f = keep_slot(P, status, key, i, m, own_lo, own_hi, blk);
+      keep[i] = f ? 1u : 0u;
+      c += f ? 1u : 0u;
+    }
+  }
+  const unsigned tot = block_sum256(c, ws);
+  if (threadIdx.x == 0) tile[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_keep_scan(unsigned* __restrict__ tile, const unsigned* __restrict__ n,
+                                                    int cap) {
+  __shared__ unsigned ws[16];
+  const int m = (int)min(*n, (unsigned)cap);
+  const int nt = min((cap + kKeepTile - 1) / kKeepTile, m / kKeepTile + 1);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned carry = 0;
+  for (int b0 = 0; b0 < nt; b0 += 1024) {
+    const int b = b0 + (int)threadIdx.x;
+    const unsigned v = b < nt ? tile[b] : 0u;
+    unsigned x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned t = __shfl_up(x, d, 64);
+      if (lane >= d) x += t;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    unsigned before = 0, all = 0;
+    for (int q = 0; q < 16; ++q) {
+      before += q < w ? ws[q] : 0u;
+      all += ws[q];
+    }
+    if (b < nt) tile[b] = carry + before + x - v;
+    carry += all;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_keep_scatter(const unsigned* __restrict__ keep, const unsigned* __restrict__ tile,
+                                                      const Keypoint* __restrict__ kp, const unsigned* __restrict__ n,
+                                                      int cap, unsigned* __restrict__ pos, Keypoint* __restrict__ out) {
+  const int m = (int)min(*n, (unsigned)cap);
+  const int t0 = blockIdx.x * kKeepTile;
+  if (t0 > m) return;
+  __shared__ unsigned ws[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  unsigned carry = tile[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kKeepTile / 256; ++k) {
+    const int i = t0 + k * 256 + (int)threadIdx.x;
+    const bool f = i < cap && keep[i] != 0u;
+    const unsigned long long bal = __ballot(f);
+    if (lane == 0) ws[k & 1][w] = (unsigned)__popcll(bal);
+    __syncthreads();
+    unsigned off = carry;
+    for (int q = 0; q < w; ++q) off += ws[k & 1][q];
+    const unsigned p = off + (unsigned)__popcll(bal & below);
+    if (i < cap) pos[i] = p;
+    if (f && i < m) out[p] = kp[i];
+    carry += ws[k & 1][0] + ws[k & 1][1] + ws[k & 1][2] + ws[k & 1][3];
+  }
 }
 
 // keep: k_status_to_keep's flags (kept keypoint, in the owned rows).
@@ -494,6 +598,18 @@ hipError_t launch_status_to_keep(const Pyramid& P, const int* status, const unsi
   if (cap <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_status_to_keep, dim3((cap + 255) / 256), dim3(256), 0, st, P, status, key, keep, n, cap,
                      own_lo, own_hi, blk);
+  return hipGetLastError();
+}
+
+hipError_t launch_keep_compact(const Pyramid& P, const int* status, const unsigned* key, unsigned* keep,
+                               unsigned* pos, unsigned* tile, const unsigned* n, int cap, int own_lo, int own_hi,
+                               unsigned* blk, const Keypoint* kp, Keypoint* out, hipStream_t st) {
+  if (cap <= 0) return hipSuccess;
+  const int nt = (int)keep_tiles(cap);
+  hipLaunchKernelGGL(k_keep_flags, dim3(nt), dim3(256), 0, st, P, status, key, keep, n, cap, own_lo, own_hi, blk,
+                     tile);
+  hipLaunchKernelGGL(k_keep_scan, dim3(1), dim3(1024), 0, st, tile, n, cap);
+  hipLaunchKernelGGL(k_keep_scatter, dim3(nt), dim3(256), 0, st, keep, tile, kp, n, cap, pos, out);
   return hipGetLastError();
 }
 
