@@ -1061,6 +1061,7 @@ static int extrema_finish(sift_ctx* ctx) {
     E.n_out = cnt + kCntN;  // the list's length, written by k_emit (no 4-byte copy launch)
     E.n_index = rows;
     E.n_oct = P.O;
+    E.o_first = std::min(std::max(ctx->o_first, ctx->scan_first), P.O - 1);  // rows of earlier octaves hold no decisions
     for (int o = 0; o < P.O; ++o) {
       E.row_off[o] = (int)ctx->x_row_off[o];
       E.word_off[o] = ctx->x_word_off[o];
@@ -1100,6 +1101,7 @@ static int extrema_finish(sift_ctx* ctx) {
     E.n_out = cnt + kCntLowSure;
     E.n_index = rows;
     E.n_oct = P.O;
+    E.o_first = std::min(std::max(ctx->o_first, ctx->scan_first), P.O - 1);  // rows of earlier octaves hold no decisions
     for (int o = 0; o < P.O; ++o) {
       E.row_off[o] = (int)ctx->x_row_off[o];
       E.word_off[o] = ctx->x_word_off[o];

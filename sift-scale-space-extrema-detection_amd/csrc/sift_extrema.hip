@@ -508,11 +508,13 @@ __global__ __launch_bounds__(256, SIFT_XMINW) void k_extrema(const Pyramid P, co
 __global__ __launch_bounds__(256) void k_emit(const Pyramid P, const EmitLaunch E) {
   if (E.n_out && blockIdx.x == 0 && threadIdx.x == 0) *E.n_out = E.rowoff[E.n_index];
   const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);  // global row (image-major)
   const int rpi = E.row_off[E.n_oct];
-  if (g >= rpi * P.nimg) return;
-  const int im = g / rpi, gl = g - im * rpi;
-  int o = 0;
+  const int r0 = E.row_off[E.o_first], act = rpi - r0;  // rows per image with decisions
+  const int ga = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ga >= act * P.nimg) return;
+  const int im = ga / act, gl = r0 + (ga - im * act);
+  const int g = im * rpi + gl;  // global row (image-major)
+  int o = E.o_first;
   while (o + 1 < E.n_oct && gl >= E.row_off[o + 1]) ++o;
   const Octave& oc = P.oct[o];
   const int h = oc.h, w = oc.w;
@@ -835,7 +837,8 @@ hipError_t launch_extrema(const Pyramid& P, ExtremaLaunch& L, hipStream_t st, in
 }
 
 hipError_t launch_emit(const Pyramid& P, const EmitLaunch& E, hipStream_t st) {
-  const int rows = E.row_off[E.n_oct] * std::max(1, P.nimg);
+  if (E.o_first < 0 || E.o_first >= E.n_oct) return hipErrorInvalidValue;
+  const int rows = (E.row_off[E.n_oct] - E.row_off[E.o_first]) * std::max(1, P.nimg);
   hipLaunchKernelGGL(k_emit, dim3(std::max(1, (rows + 3) / 4)), dim3(256), 0, st, P, E);
   return hipGetLastError();
 }

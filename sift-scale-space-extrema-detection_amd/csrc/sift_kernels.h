@@ -148,6 +148,7 @@ constexpr int kPatchFloats = 20;
 // (s-1) h_o + y.
 struct EmitLaunch {
   int n_oct;
+  int o_first;                   // first octave with decisions (earlier octaves' rows hold none: no waves)
   int row_off[kMaxOctaves + 1];  // first global row of each octave ([S][h] rows per octave)
   long long word_off[kMaxOctaves];  // first bitmap word of each octave
   int nw[kMaxOctaves];
