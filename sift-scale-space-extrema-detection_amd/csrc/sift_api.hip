@@ -533,7 +533,13 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
       return set_err(ctx, SIFT_E_UNSUPPORTED, "blur radius too large for one LDS strip");
   if (need_weights) {
     // Upload only when the taps changed (the same schedule image after image).
-    if (w != ctx->wts_host || !ctx->wts.p) {
+    // The taps are laid out octave after octave, so a schedule with fewer
+    // octaves is a prefix of a deeper one: a context that alternates row bands
+    // (octaves 0..K) and tail pieces (octaves 0..t) keeps the deepest taps
+    // and uploads (a blocking copy) only when a deeper schedule arrives.
+    const bool prefix = w.size() <= ctx->wts_host.size() &&
+                        std::equal(w.begin(), w.end(), ctx->wts_host.begin());
+    if (!prefix || !ctx->wts.p) {
       if (ctx->wts.ensure(w.size() * sizeof(double)) != hipSuccess)
         return set_err(ctx, SIFT_E_HIP, "hipMalloc weights");
       if (hipMemcpy(ctx->wts.p, w.data(), w.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
