@@ -325,7 +325,7 @@ hipError_t launch_scatter_keys(const unsigned* keep, const unsigned* pos, const 
 #ifndef SIFT_KEEP_SCAN
 #define SIFT_KEEP_SCAN 1  // 0: capacity-sized device scan (the round-4 compaction; A/B builds)
 #endif
-constexpr int kKeepTile = 2048;
+constexpr int kKeepTile = 512;  // two slots per thread: 4K (714 K candidates) 1400 tiles
 inline size_t keep_tiles(int cap) { return cap > 0 ? (size_t)(cap + kKeepTile - 1) / kKeepTile : 0; }
 hipError_t launch_keep_compact(const Pyramid& P, const int* status, const unsigned* key, unsigned* keep,
                                unsigned* pos, unsigned* tile, const unsigned* n, int cap, int own_lo, int own_hi,
