@@ -1311,7 +1311,10 @@ static int refine_enqueue(sift_ctx* ctx) {
     HIPCHK(launch_refine_fast(P, R, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev_heavy, ctx->stream));  // the rest is latency-bound tail work
     // Uncertain decisions exist only with fp32-rounded native planes.
-    R.wide_exact = ctx->o_first > 0;  // a tail piece (sift_detect_from_seed*): latency over throughput
+#ifndef SIFT_WIDE_EXACT
+#define SIFT_WIDE_EXACT 0  // 1: 256-thread exact refinement for whole images too (A/B builds)
+#endif
+    R.wide_exact = SIFT_WIDE_EXACT || ctx->o_first > 0;  // a tail piece (sift_detect_from_seed*): latency over throughput
     if (ctx->dog_source == kNative) HIPCHK(launch_refine_exact(P, R, ctx->stream));
 #if SIFT_KEEP_SCAN
     HIPCHK(ctx->keep_tile.ensure(keep_tiles(cap) * sizeof(unsigned)));
