@@ -8,7 +8,7 @@ const raw = fs.readFileSync(inPath);
 const image = { width: W, height: H, data: new Float32Array(raw.buffer, raw.byteOffset, W * H) };
 const base = { number_of_octaves: 4, scales_per_octave: 5, format: fmt };
 (async () => {
-  for (const inflight of [3, 4, 3, 4, 3, 4]) {
+  for (const inflight of (process.env.POOLS || "3,4,3,4,3,4").split(",").map(Number)) {
     const o = { ...base, inflight };
     await Promise.all(Array.from({ length: inflight }, () => sift.detectAsync(image, o)));
     const t0 = performance.now();
