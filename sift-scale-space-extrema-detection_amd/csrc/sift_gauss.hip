@@ -1730,6 +1730,11 @@ static void set_attr() {
 // k_seed_vert forms the vertical sums of the even rows (every column),
 // k_seed_horz the horizontal sums at the even columns.  3/8 of one scale's
 // work instead of all S+3 scales with their planes.
+#ifndef SIFT_SEED_BATCH
+#define SIFT_SEED_BATCH 8  // 16 measured the same (r5aq: 34.7 vs 35.2 us at 8K octave 3)
+#endif
+constexpr int kSeedBatch = SIFT_SEED_BATCH;
+
 __global__ __launch_bounds__(256) void k_seed_vert(const Pyramid P, int o, const double* __restrict__ base,
                                                    double* __restrict__ vrow) {
   const Octave& oc = P.oct[o];
@@ -1739,15 +1744,16 @@ __global__ __launch_bounds__(256) void k_seed_vert(const Pyramid P, int o, const
   const double* __restrict__ wt = P.wts + oc.wofs[P.S];
   const double* __restrict__ col = base + x;
   const long long w = oc.w;
-  // eight loads in flight ahead of their fma steps (the chain's order is kept)
+  // kSeedBatch loads in flight ahead of their fma steps (the chain's order is
+  // kept): 95 taps at r = 47 are 6 dependent load rounds instead of 95
   double acc = 0.0;
   int j = 0;
-  for (; j + 8 <= 2 * r + 1; j += 8) {
-    double v[8];
+  for (; j + kSeedBatch <= 2 * r + 1; j += kSeedBatch) {
+    double v[kSeedBatch];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = col[clampi(2 * yp + j + k - r, 0, h - 1) * w];
+    for (int k = 0; k < kSeedBatch; ++k) v[k] = col[clampi(2 * yp + j + k - r, 0, h - 1) * w];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc = __builtin_fma(wt[j + k], v[k], acc);
+    for (int k = 0; k < kSeedBatch; ++k) acc = __builtin_fma(wt[j + k], v[k], acc);
   }
   for (; j <= 2 * r; ++j) acc = __builtin_fma(wt[j], col[clampi(2 * yp + j - r, 0, h - 1) * w], acc);
   vrow[(long long)yp * w + x] = acc;
@@ -1764,12 +1770,12 @@ __global__ __launch_bounds__(256) void k_seed_horz(const Pyramid P, int o, const
   const double* __restrict__ row = vrow + (long long)yp * w;
   double acc = 0.0;
   int i = 0;
-  for (; i + 8 <= 2 * r + 1; i += 8) {
-    double v[8];
+  for (; i + kSeedBatch <= 2 * r + 1; i += kSeedBatch) {
+    double v[kSeedBatch];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = row[clampi(2 * xp + i + k - r, 0, w - 1)];
+    for (int k = 0; k < kSeedBatch; ++k) v[k] = row[clampi(2 * xp + i + k - r, 0, w - 1)];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc = __builtin_fma(wt[i + k], v[k], acc);
+    for (int k = 0; k < kSeedBatch; ++k) acc = __builtin_fma(wt[i + k], v[k], acc);
   }
   for (; i <= 2 * r; ++i) acc = __builtin_fma(wt[i], row[clampi(2 * xp + i - r, 0, w - 1)], acc);
   next[(long long)yp * nw + xp] = acc;
