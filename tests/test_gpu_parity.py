@@ -577,6 +577,34 @@ def test_owned_rows_and_block_counts(gpu_ctx):
         np.testing.assert_array_equal(counts, np.bincount(org[keep, 0] * S + org[keep, 1] - 1, minlength=O * S))
 
 
+def test_compaction_after_a_larger_detection_and_empty_band(gpu_ctx):
+    """The keypoint compaction works only on the slot tiles up to the device
+    candidate count (launch_keep_compact): a small detection right after a
+    large one on the same context (stale flags and positions past its count)
+    gives the fresh context's records, origins and block counts, and a band
+    that owns no rows keeps nothing."""
+    p = sift_amd.make_params(4, 4, flags=sift_amd.F_KEYPOINT_ORIGINS)
+    small = blob_image(200, 150, seed=5)
+    with sift_amd.Context(0) as fresh:
+        want = fresh.detect(small, p).copy()
+        want_org = fresh.keypoint_origins().copy()
+        want_blk = fresh.block_counts().copy()
+    assert len(want) > 0
+    gpu_ctx.detect(blob_image(1024, 768, seed=3), p)
+    got = gpu_ctx.detect(small, p).copy()
+    assert got.tobytes() == want.tobytes()
+    np.testing.assert_array_equal(gpu_ctx.keypoint_origins(), want_org)
+    np.testing.assert_array_equal(gpu_ctx.block_counts(), want_blk)
+    gpu_ctx.set_owned_rows(10 ** 6, -1)
+    try:
+        none = gpu_ctx.detect(small, p).copy()
+        blk = gpu_ctx.block_counts().copy()
+    finally:
+        gpu_ctx.set_owned_rows(-1)
+    assert len(none) == 0
+    assert not blk.any()
+
+
 @pytest.mark.parametrize("t", [3, 5])
 def test_range_detection_seed_only_octaves_bit_identical(gpu_ctx, t):
     """sift_detect_from_seed_range_device evaluates the octaves below its scan
