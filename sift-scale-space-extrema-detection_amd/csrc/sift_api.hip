@@ -779,12 +779,21 @@ static void read_gauss_times(sift_ctx* ctx) {
   }
 }
 
+// A page-locked caller image is uploaded by one DMA straight from the
+// caller's memory (build_common), which every host-image entry point waits
+// for before it returns -- on its error exits too, so the caller
+// may free or overwrite the image as soon as the call returns.
+static int host_image_exit(sift_ctx* ctx, int rc) {
+  if (rc != SIFT_OK && ctx && ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  return rc;
+}
+
 extern "C" {
 
 int sift_build_scale_space(sift_ctx* ctx, const float* img, int width, int height, size_t stride_px,
                            const sift_params* p, const double* sig) {
   int rc = build_common(ctx, img, nullptr, width, height, stride_px, p, sig);
-  if (rc) return rc;
+  if (rc) return host_image_exit(ctx, rc);
   HIPCHK(hipStreamSynchronize(ctx->stream));
   float a = 0;
   (void)hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
@@ -1702,7 +1711,7 @@ int sift_detect_batch(sift_ctx* ctx, const float* imgs, int n_images, size_t ima
   if (ctx->detect_pending || ctx->begin_pending)
     return set_err(ctx, SIFT_E_STATE, "a detection is already in flight on this context");
   const int rc = detect_enqueue(ctx, imgs, nullptr, width, height, stride_px, p, n_images, image_stride_px);
-  return rc ? rc : detect_finish(ctx, out, cap, n_out);
+  return host_image_exit(ctx, rc ? rc : detect_finish(ctx, out, cap, n_out));
 }
 
 int sift_detect_batch_device(sift_ctx* ctx, const float* d_imgs, int n_images, size_t image_stride_px, int width,
@@ -1736,7 +1745,7 @@ int sift_detect_wait(sift_ctx* ctx, sift_keypoint* out, size_t cap, size_t* n_ou
 int sift_detect(sift_ctx* ctx, const float* img, int width, int height, size_t stride_px, const sift_params* p,
                 sift_keypoint* out, size_t cap, size_t* n_out) {
   if (ctx) (void)hipSetDevice(ctx->device);
-  return detect_common(ctx, img, nullptr, width, height, stride_px, p, out, cap, n_out);
+  return host_image_exit(ctx, detect_common(ctx, img, nullptr, width, height, stride_px, p, out, cap, n_out));
 }
 
 int sift_detect_device(sift_ctx* ctx, const float* d_img, int width, int height, size_t stride_px,

@@ -48,21 +48,14 @@ static napi_value throw_sift(napi_env env, struct sift_ctx *ctx, int rc, const c
 /* The JS handle of a context.  A sift_ctx is not re-entrant (include/sift_hip.h):
  * while a detectAsync job runs on the libuv pool the context is `busy` and
  * every other call on it is rejected instead of racing the worker thread. */
-typedef struct {
+typedef struct ctx_box {
   struct sift_ctx *ctx;
   int busy;
   int flags;       /* sift_params.flags of the last build / load through this handle */
   double d2h_ms;   /* host wall time of this context's last keypoint copy (JS thread only) */
+  napi_ref weak;   /* weak reference to the JS handle (no finalizer: see pool_rec) */
+  struct ctx_box *next;
 } ctx_box;
-
-static void ctx_finalize(napi_env env, void *data, void *hint) {
-  (void)env;
-  (void)hint;
-  ctx_box *b = (ctx_box *)data;
-  if (!b) return;
-  if (b->ctx) sift_ctx_destroy(b->ctx);
-  free(b);
-}
 
 static ctx_box *get_box(napi_env env, napi_value v) {
   void *p = NULL;
@@ -321,9 +314,14 @@ static void pool_give(void *p, size_t bytes) {
   if (p) big_free(p, cls);
 }
 
+typedef struct env_state env_state;
+static env_state *get_state(napi_env env);
+static void pool_sweep(napi_env env, env_state *st);
+
 /* Pool state for the tests: buffers, bytes, page-locked buffers, bytes. */
 static napi_value js_pool_stats(napi_env env, napi_callback_info info) {
   (void)info;
+  pool_sweep(env, get_state(env));  /* collected results count as pooled */
   pthread_mutex_lock(&g_pool_mu);
   const double v[4] = {(double)g_pool_n, (double)g_pool_bytes, (double)g_reg_n, (double)g_reg_bytes};
   pthread_mutex_unlock(&g_pool_mu);
@@ -337,77 +335,146 @@ static napi_value js_pool_stats(napi_env env, napi_callback_info info) {
   return arr;
 }
 
-/* One external ArrayBuffer over a pool buffer.  `released`: the caller handed
- * it back early (releaseBuffer: detached, returned to the pool); the
- * finalizer then only frees the record. */
-typedef struct {
+/* Result-buffer ownership.  Node 12 defers every N-API finalizer that a
+ * collection triggers to a native immediate, and its environment teardown
+ * can run those after the napi_env is gone (a fault opening a HandleScope,
+ * profiles/r5ag_node12_exit_finalizer.txt) or meet an external ArrayBuffer
+ * whose finalizer is still queued (`ArrayBufferReference::Finalize`
+ * assertion).  So no object this addon hands out carries a finalizer: a
+ * pooled result is an external ArrayBuffer WITHOUT one, and this record --
+ * the single owner of its memory -- holds a weak reference to it.  A record
+ * whose ArrayBuffer V8 has collected is swept (memory back to the pool, V8's
+ * external-memory count lowered) whenever the environment makes a new pooled
+ * result, and at the environment's cleanup hook.  Records are touched on
+ * their environment's JS thread only. */
+typedef struct pool_rec {
   void *p;
   size_t bytes;
-  int released;
+  napi_ref weak;         /* weak reference to the ArrayBuffer (no finalizer) */
+  int released;          /* the memory went back early (releaseBuffer) */
+  int borrows;           /* detectAsync jobs reading this memory on the libuv pool */
+  int give_pending;      /* released while borrowed: give when the last borrow ends */
+  struct pool_rec *next;
 } pool_rec;
 
-/* Set by the environment's cleanup hook: the finalizers that follow (the
- * environment's teardown runs every pending one) leave V8's accounting alone. */
-static volatile int g_env_closing = 0;
+/* Per-environment state (napi_set_instance_data): main thread and every
+ * worker_threads Worker have their own. */
+struct env_state {
+  pool_rec *live;        /* result buffers handed to JS and not yet swept */
+  ctx_box *ctxs;         /* contexts handed to JS and not yet swept */
+  int closing;           /* this environment's cleanup hook has run */
+};
 
-static void pool_finalize(napi_env env, void *data, void *hint) {
-  (void)data;
-  pool_rec *r = (pool_rec *)hint;
-  if (!r->released) {
-    if (!g_env_closing) {
-      int64_t adj;
-      napi_adjust_external_memory(env, -(int64_t)r->bytes, &adj);
-    }
-    pool_give(r->p, r->bytes);
+static env_state *get_state(napi_env env) {
+  void *d = NULL;
+  if (napi_get_instance_data(env, &d) != napi_ok) return NULL;
+  return (env_state *)d;
+}
+
+/* The memory of a record goes back to the pool (once, and not while a job reads it). */
+static void rec_give(pool_rec *r) {
+  if (r->borrows > 0) {
+    r->give_pending = 1;
+    return;
   }
-  free(r);
+  r->give_pending = 0;
+  if (r->p) pool_give(r->p, r->bytes);
+  r->p = NULL;
+}
+
+/* Sweep the records whose ArrayBuffers V8 has collected. */
+static void pool_sweep(napi_env env, env_state *st) {
+  if (!st || st->closing) return;
+  napi_handle_scope scope;
+  if (napi_open_handle_scope(env, &scope) != napi_ok) return;
+  int64_t freed = 0;
+  for (pool_rec **pp = &st->live; *pp;) {
+    pool_rec *r = *pp;
+    napi_value v = NULL;
+    if (r->borrows == 0 && napi_get_reference_value(env, r->weak, &v) == napi_ok && v == NULL) {
+      *pp = r->next;
+      napi_delete_reference(env, r->weak);
+      if (!r->released) {
+        freed += (int64_t)r->bytes;
+        rec_give(r);
+      }
+      free(r);
+    } else {
+      pp = &r->next;
+    }
+  }
+  napi_close_handle_scope(env, scope);
+  if (freed) {
+    int64_t adj;
+    napi_adjust_external_memory(env, -freed, &adj);
+  }
+}
+
+/* The live, unreleased record whose memory starts at p (NULL: not a pooled result). */
+static pool_rec *pool_find(env_state *st, const void *p) {
+  if (!st || !p) return NULL;
+  for (pool_rec *r = st->live; r; r = r->next)
+    if (!r->released && r->p == p) return r;
+  return NULL;
 }
 
 /* An external ArrayBuffer over a pool buffer (takes ownership of p, also on failure). */
 static napi_value pool_arraybuffer(napi_env env, void *p, size_t bytes) {
+  env_state *st = get_state(env);
+  pool_sweep(env, st);
   napi_value ab;
-  pool_rec *r = (pool_rec *)malloc(sizeof(pool_rec));
-  if (!r) {
+  pool_rec *r = (pool_rec *)calloc(1, sizeof(pool_rec));
+  if (!st || !r) {
+    free(r);
     pool_give(p, bytes);
     return NULL;
   }
   r->p = p;
   r->bytes = bytes;
-  r->released = 0;
-  if (napi_create_external_arraybuffer(env, p, bytes, pool_finalize, r, &ab) != napi_ok) {
+  if (napi_create_external_arraybuffer(env, p, bytes, NULL, NULL, &ab) != napi_ok ||
+      napi_create_reference(env, ab, 0, &r->weak) != napi_ok) {
     free(r);
     pool_give(p, bytes);
     return NULL;
   }
-  /* the record travels with the object: releaseBuffer finds it */
-  if (napi_wrap(env, ab, r, NULL, NULL, NULL) != napi_ok) r->released = -1; /* not releasable early */
+  r->next = st->live;
+  st->live = r;
   int64_t adj;
   napi_adjust_external_memory(env, (int64_t)bytes, &adj);
   return ab;
 }
 
+/* The pooled result an ArrayBuffer is (NULL for any other buffer). */
+static pool_rec *pool_rec_of(napi_env env, napi_value ab) {
+  bool isab = false;
+  void *data = NULL;
+  size_t len = 0;
+  if (napi_is_arraybuffer(env, ab, &isab) != napi_ok || !isab) return NULL;
+  if (napi_get_arraybuffer_info(env, ab, &data, &len) != napi_ok) return NULL;
+  pool_rec *r = pool_find(get_state(env), data);
+  return r && r->bytes == len ? r : NULL;
+}
+
 /* releaseBuffer(arrayBuffer) -> bool: hand a pooled result buffer (a plane or
  * a typed keypoint field of >= 1 MiB) back before V8 collects it: the
  * ArrayBuffer is detached (its views read as empty from then on) and the
- * memory returns to the pool at once, so the next result of its size class
- * reuses it -- page-locked on reuse -- instead of faulting in fresh pages.
- * false for any other buffer (left untouched). */
+ * memory returns to the pool -- at once, or, while a detectAsync job still
+ * reads it as its input image, when that job completes -- so the next result
+ * of its size class reuses it (page-locked on reuse) instead of faulting in
+ * fresh pages.  false for any other buffer and for one released before (left
+ * untouched). */
 static napi_value js_release_buffer(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1], res;
   NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  bool ok = false, isab = false;
-  void *w = NULL;
-  if (argc > 0 && napi_is_arraybuffer(env, argv[0], &isab) == napi_ok && isab &&
-      napi_unwrap(env, argv[0], &w) == napi_ok && w) {
-    pool_rec *r = (pool_rec *)w;
-    if (r->released == 0 && napi_detach_arraybuffer(env, argv[0]) == napi_ok) {
-      r->released = 1;
-      int64_t adj;
-      napi_adjust_external_memory(env, -(int64_t)r->bytes, &adj);
-      pool_give(r->p, r->bytes);
-      ok = true;
-    }
+  bool ok = false;
+  pool_rec *r = argc > 0 ? pool_rec_of(env, argv[0]) : NULL;
+  if (r && napi_detach_arraybuffer(env, argv[0]) == napi_ok) {
+    r->released = 1;
+    int64_t adj;
+    napi_adjust_external_memory(env, -(int64_t)r->bytes, &adj);
+    rec_give(r);
+    ok = true;
   }
   NAPI_CALL(env, napi_get_boolean(env, ok, &res));
   return res;
@@ -417,12 +484,55 @@ static napi_value js_release_buffer(napi_env env, napi_callback_info info) {
 static napi_value make_typed_pooled(napi_env env, napi_typedarray_type t, size_t n, size_t elem, void **data) {
   const size_t bytes = n * elem;
   if (bytes < POOL_MIN_BYTES) return make_typed(env, t, n, elem, data);
+  pool_sweep(env, get_state(env));  /* collected results first, so this request can reuse one */
   void *p = pool_take(bytes);
   if (!p) return NULL;
   napi_value ab = pool_arraybuffer(env, p, bytes), arr;
   if (!ab || napi_create_typedarray(env, t, n, ab, 0, &arr) != napi_ok) return NULL;
   if (data) *data = p;
   return arr;
+}
+
+/* poolBuffer(bytes) -> Float32Array over a pooled buffer (test hook: the
+ * result-buffer lifetime without a device). */
+static napi_value js_pool_buffer(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  double b = 0;
+  if (argc > 0) napi_get_value_double(env, argv[0], &b);
+  if (!(b >= 4)) {
+    napi_throw_range_error(env, NULL, "poolBuffer: bytes >= 4");
+    return NULL;
+  }
+  float *d = NULL;
+  napi_value arr = make_typed_pooled(env, napi_float32_array, (size_t)b / 4, 4, (void **)&d);
+  if (!arr) {
+    napi_throw_error(env, NULL, "poolBuffer: allocation failed");
+    return NULL;
+  }
+  return arr;
+}
+
+/* Destroy the contexts whose JS handles V8 has collected (a busy one is
+ * still referenced by its job, so it is never collected). */
+static void ctx_sweep(napi_env env, env_state *st) {
+  if (!st || st->closing) return;
+  napi_handle_scope scope;
+  if (napi_open_handle_scope(env, &scope) != napi_ok) return;
+  for (ctx_box **pp = &st->ctxs; *pp;) {
+    ctx_box *b = *pp;
+    napi_value v = NULL;
+    if (!b->busy && napi_get_reference_value(env, b->weak, &v) == napi_ok && v == NULL) {
+      *pp = b->next;
+      napi_delete_reference(env, b->weak);
+      if (b->ctx) sift_ctx_destroy(b->ctx);
+      free(b);
+    } else {
+      pp = &b->next;
+    }
+  }
+  napi_close_handle_scope(env, scope);
 }
 
 /* createContext(device) -> external */
@@ -442,12 +552,18 @@ static napi_value js_create_context(napi_env env, napi_callback_info info) {
     return NULL;
   }
   b->ctx = ctx;
+  env_state *st = get_state(env);
+  ctx_sweep(env, st);
   napi_value ext;
-  if (napi_create_external(env, b, ctx_finalize, NULL, &ext) != napi_ok) {
-    ctx_finalize(env, b, NULL);
+  if (!st || napi_create_external(env, b, NULL, NULL, &ext) != napi_ok ||
+      napi_create_reference(env, ext, 0, &b->weak) != napi_ok) {
+    sift_ctx_destroy(ctx);
+    free(b);
     napi_throw_error(env, NULL, "napi_create_external failed");
     return NULL;
   }
+  b->next = st->ctxs;
+  st->ctxs = b;
   return ext;
 }
 
@@ -860,6 +976,7 @@ typedef struct {
   sift_params p;
   size_t n;
   kp_soa kp;          /* host field arrays, copied on the worker thread */
+  pool_rec *borrowed; /* the input image is a pooled result: held against release until completion */
   double d2h_ms;      /* their copy's wall time, published to the context on the JS thread */
 } detect_job;
 
@@ -901,6 +1018,7 @@ static void detect_complete(napi_env env, napi_status status, void *data) {
     if (j->kp.ints) pool_give(j->kp.ints, sizeof(int32_t) * 4 * n);
     if (j->kp.reals) pool_give(j->kp.reals, sizeof(double) * 4 * n);
   }
+  if (j->borrowed && --j->borrowed->borrows == 0 && j->borrowed->give_pending) rec_give(j->borrowed);
   napi_delete_reference(env, j->img_ref);
   napi_delete_reference(env, j->ctx_ref);
   napi_delete_async_work(env, j->work);
@@ -938,6 +1056,18 @@ static napi_value js_detect_async(napi_env env, napi_callback_info info) {
   NAPI_CALL(env, napi_create_async_work(env, NULL, name, detect_execute, detect_complete, j, &j->work));
   NAPI_CALL(env, napi_queue_async_work(env, j->work));
   box->busy = 1;  /* until detect_complete (JS thread) */
+  {
+    /* an input that is a pooled result (a plane handed out earlier) stays
+     * ours until the job is done: releaseBuffer then defers its give */
+    napi_typedarray_type t;
+    size_t n, off;
+    void *d;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, argv[1], &t, &n, &d, &ab, &off) == napi_ok) {
+      j->borrowed = pool_rec_of(env, ab);
+      if (j->borrowed) j->borrowed->borrows++;
+    }
+  }
   return promise;
 }
 
@@ -1113,9 +1243,33 @@ static void segv_trace(int sig) {
   raise(sig);
 }
 
+/* The environment is going away (process exit or a Worker ending; no JS runs
+ * from here on): its result buffers go back to the pool and its contexts are
+ * destroyed, except what an unfinished detectAsync job still uses. */
 static void on_env_cleanup(void *arg) {
-  (void)arg;
-  g_env_closing = 1;
+  napi_env env = (napi_env)arg;
+  env_state *st = get_state(env);
+  if (!st) return;
+  st->closing = 1;
+  for (pool_rec *r = st->live, *nx; r; r = nx) {
+    nx = r->next;
+    napi_delete_reference(env, r->weak);
+    if (r->borrows > 0) continue;  /* its job's memory: left as it is */
+    if (!r->released || r->give_pending) {
+      r->borrows = 0;
+      rec_give(r);
+    }
+    free(r);
+  }
+  st->live = NULL;
+  for (ctx_box *b = st->ctxs, *nx; b; b = nx) {
+    nx = b->next;
+    napi_delete_reference(env, b->weak);
+    if (b->busy) continue;
+    if (b->ctx) sift_ctx_destroy(b->ctx);
+    free(b);
+  }
+  st->ctxs = NULL;
 }
 
 /* At exit (before the HIP runtime's own teardown, whose handlers were
@@ -1133,7 +1287,15 @@ static void pool_atexit(void) {
 }
 
 static napi_value init(napi_env env, napi_value exports) {
-  napi_add_env_cleanup_hook(env, on_env_cleanup, NULL);
+  {
+    env_state *st = (env_state *)calloc(1, sizeof(env_state));
+    if (!st || napi_set_instance_data(env, st, NULL, NULL) != napi_ok) {
+      free(st);
+      napi_throw_error(env, NULL, "sift_napi: per-environment state");
+      return NULL;
+    }
+    napi_add_env_cleanup_hook(env, on_env_cleanup, env);
+  }
   {
     static int once = 0;
     if (!once) {
@@ -1166,6 +1328,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"detectAsync", 0, js_detect_async, 0, 0, 0, napi_enumerable, 0},
       {"poolStats", 0, js_pool_stats, 0, 0, 0, napi_enumerable, 0},
       {"releaseBuffer", 0, js_release_buffer, 0, 0, 0, napi_enumerable, 0},
+      {"poolBuffer", 0, js_pool_buffer, 0, 0, 0, napi_enumerable, 0},
       {"detectBatch", 0, js_detect_batch, 0, 0, 0, napi_enumerable, 0},
       {"counts", 0, js_counts, 0, 0, 0, napi_enumerable, 0},
       {"timings", 0, js_timings, 0, 0, 0, napi_enumerable, 0},

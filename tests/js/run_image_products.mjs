@@ -65,4 +65,3 @@ out.worker = {
 };
 out.gaussPlane00 = Array.from(wss[0][0].image[0].slice(0, 4));
 fs.writeFileSync(outPath, JSON.stringify(out));
-process.exit(0);  // skip Node 12's teardown of queued N-API finalizers (profiles/r5ag_node12_exit_finalizer.txt)

