@@ -199,9 +199,10 @@ def main():
                          "detections per step")
     ap.add_argument("--inflight", type=int, default=None,
                     help="detections in flight per GPU (one context each; the host settles image k while "
-                         "image k+1 runs).  Default: 2 for single images of >= 4 Mpix (4K: 2 > 3 by 1.5-2 %%, "
-                         "profiles/r4am_inflight_ab.txt), 3 for smaller ones (1080p: +15 %%, "
-                         "profiles/r5h_cfg2_inflight.txt) and for batched launches (cfg 4: 3 > 2 by 3 %%, DESIGN 8a)")
+                         "image k+1 runs).  Default under --overlap full (the default schedule): 3 for single "
+                         "images of >= 4 Mpix (4K: 3 > 4 by 1-2 %%, profiles/r5w_schedule_ab.txt), 4 for smaller "
+                         "images and batched launches when GPU_MAX_HW_QUEUES >= 8, else 3; under an ordered "
+                         "--overlap: 2 for single images of >= 4 Mpix (profiles/r4am_inflight_ab.txt), 3 otherwise")
     ap.add_argument("--overlap", default=None,
                     choices=["none", "octave0", "gaussian", "refinement", "full", "phased"],
                     help="how consecutive images overlap on the GPU: none = contexts share one stream; "
@@ -233,10 +234,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            print("bench.py: --gpus %d needs torchrun with %d processes" % (args.gpus, args.gpus), file=sys.stderr)
-            return 2
+    if world != args.gpus:
+        # the driver launches N ranks for --gpus N; any other pairing would report a wrong n_gpus
+        print("bench.py: --gpus %d but WORLD_SIZE=%d: launch %d processes (torchrun --nproc-per-node %d)"
+              % (args.gpus, world, args.gpus, args.gpus), file=sys.stderr)
+        return 2
 
     import numpy as np
     import torch

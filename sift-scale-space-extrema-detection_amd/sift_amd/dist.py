@@ -86,7 +86,7 @@ class PipelinedKeypointGather:
         self.group = group
         self.world = dist.get_world_size(group)
         self.depth = max(1, int(depth))
-        self.slots = [{"cap": 0, "send": None, "recv": None, "work": None, "counts": None}
+        self.slots = [{"cap": 0, "send": None, "recv": None, "work": None, "counts": None, "m": 0}
                       for _ in range(self.depth)]
         self.k = 0
 
@@ -113,7 +113,13 @@ class PipelinedKeypointGather:
             slot["cap"] = cap
         n = fill(slot["send"], slot["cap"])
         assert n == n_local, (n, n_local)
-        slot["work"] = dist.all_gather_into_tensor(slot["recv"], slot["send"], group=self.group, async_op=True)
+        # only the step's largest count goes on the wire (the buffers keep
+        # 1/4 slack for growth; at N = 8 the slack alone would be 7 x 5 MB per
+        # 4K step): every rank receives (N - 1) x need records
+        m = need * REC
+        slot["m"] = m
+        slot["work"] = dist.all_gather_into_tensor(slot["recv"][:self.world * m], slot["send"][:m],
+                                                   group=self.group, async_op=True)
         slot["counts"] = counts
         return counts
 
@@ -129,8 +135,8 @@ class PipelinedKeypointGather:
             raise ValueError("gathered(back=%d): only the last %d step(s) are held" % (back, min(self.k, self.depth)))
         slot = self.slots[(self.k - back) % self.depth]
         self._settle(slot)
-        counts, cap = slot["counts"], slot["cap"]
-        raw = slot["recv"].view(self.world, cap * REC).cpu().numpy()
+        counts, m = slot["counts"], slot["m"]
+        raw = slot["recv"][:self.world * m].view(self.world, m).cpu().numpy()
         parts = [np.frombuffer(raw[r, :counts[r] * REC].tobytes(), dtype=KEYPOINT_DTYPE) for r in range(self.world)]
         return np.concatenate(parts) if parts else np.zeros(0, dtype=KEYPOINT_DTYPE)
 
