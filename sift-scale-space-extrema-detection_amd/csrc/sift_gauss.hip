@@ -1267,7 +1267,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
 template <int RW>
 struct RwGeom {
   static constexpr int NW = 8 + 2 * RW;              // window rows per lane
-  static constexpr int TW = RW <= 16 ? 224 : 192;     // output columns per tile
+  static constexpr int TW = RW <= 16 ? 224 : RW <= 24 ? 192 : 160;  // output columns per tile
   static constexpr int NCG = TW / 4;                  // column groups of 4
   static_assert(2 * RW <= 256 - TW, "halo fits the strip");
 };
@@ -1528,6 +1528,263 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined streamed tiles (k_gauss_rwp, round 6).  The streamed
+// k_gauss_rw<RW, true> waits for every 8-row chunk of a scale's vertical
+// window before its fmas: at 4K octave 2 a wave spends half its life in
+// s_waitcnt (r6a stall counters: wait 13.4 K of 26.4 K quad-cycles, 260
+// buffer loads in ~35 dependent rounds, 3.1 K SALU).  Here the chunks are
+// double-buffered in registers: chunk j + 1's 8 loads are issued before chunk
+// j's 64 fmas, and the last chunk of a scale issues the NEXT scale's first
+// chunk, which lands during the barrier, the horizontal pass and the stores.
+// For the compiler's waitcnt pass to count the loads exactly, every scale
+// issues the same buffer stores (a lane with nothing to store -- no item,
+// past the plane, a recomputed scale -- has its store dropped by the
+// descriptor's range check) and every chunk loads 8 rows (clamped; taps past
+// 2r are zero padding, fma(0, v, acc) == acc).  The fma chain of every output
+// is k_gauss_rw's (taps in increasing order from 0.0): bit-identical planes.
+// Interior chunks (no row clamping) take one SALU add per row.
+// Measured (r6b / r6c, experiments build, SIFT_RWP / SIFT_RWP_BIG): GPU suite
+// green with both on, but not faster -- 4K octave 2 0.091 -> 0.093-0.094 ms,
+// octave 3 (split pass + tile kernel 0.057 ms) -> 0.069-0.072 ms as one
+// k_gauss_rwp<48> launch.  The wave's s_waitcnt time fell (13.4 K -> 8.4 K
+// quad-cycles) and its issue stalls rose by as much (4.4 K -> 9.6 K): the
+// loads were not what bounded it (profiles/r6b_pipelined_streamed_ab.txt).
+// Off by default.
+// ---------------------------------------------------------------------------
+// (Row offsets on two paths, the loads after the join: the waitcnt pass
+// merges paths pessimistically, so loads issued on different paths would
+// make it wait for them one by one.)
+__device__ __forceinline__ void rwp_load(__amdgpu_buffer_rsrc_t rs, int xoff, int rb, int h, int w8, double (&v)[8]) {
+  int so[8];
+  if (rb >= 0 && rb + 7 <= h - 1) {
+    so[0] = rb * w8;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) so[k] = so[k - 1] + w8;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) so[k] = clampi(rb + k, 0, h - 1) * w8;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) asm volatile("" : "+s"(so[k]));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = load_f64(rs, xoff, so[k]);
+}
+
+// acc[t] += w[8j + k - t] v[k] over the chunk's rows k (wq = taps + 8j, zero padded).
+template <bool FIRST>
+__device__ __forceinline__ void rwp_fma(const cdouble* wq, const double (&v)[8], double (&acc)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (!(FIRST && k < t)) acc[t] = fma((double)wq[k - t], v[k], acc[t]);
+  pin(acc);
+}
+
+__device__ __forceinline__ void bstore_f64x2(__amdgpu_buffer_rsrc_t rs, int voff, double a, double b) {
+  const double2 d = make_double2(a, b);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, d), rs, voff, 0, 0);
+}
+
+// Horizontal pass of one item for radii beyond the unrolled ones (r > 24):
+// element m of the row is strip column b - D + m (b = RW - r + 4 cg, D = b & 1,
+// so the 16-byte reads are aligned), tap of output q = m - D - q; 8 elements
+// per step over zero-padded taps -- the same chain per output as rw_horz.
+// The strip columns past 255 that the last items' steps read are zero
+// (k_gauss_rwp clears them).
+template <int RW>
+__device__ __forceinline__ void rwp_horz_gen(const double* ra, const double* rb, int r, const cdouble* wp,
+                                             double (&out)[2][4]) {
+  const int D = (RW - r) & 1;
+  const double* pa = ra + (RW - r) - D;
+  const double* pb = rb + (RW - r) - D;
+  const cdouble* wq = wp - D;
+  const int nstep = (2 * r + 4 + D + 7) >> 3;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) out[0][q] = out[1][q] = 0.0;
+  for (int st = 0; st < nstep; ++st) {
+    double2 u[2][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      u[0][e] = *reinterpret_cast<const double2*>(pa + 8 * st + 2 * e);
+      u[1][e] = *reinterpret_cast<const double2*>(pb + 8 * st + 2 * e);
+    }
+    const cdouble* w8 = wq + 8 * st;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double wk = w8[m - q];
+        out[0][q] = fma(wk, (m & 1) ? u[0][m >> 1].y : u[0][m >> 1].x, out[0][q]);
+        out[1][q] = fma(wk, (m & 1) ? u[1][m >> 1].y : u[1][m >> 1].x, out[1][q]);
+      }
+    pin(out[0]);
+    pin(out[1]);
+  }
+}
+
+// L64: also store the fp64 Gaussian planes (the exact passes' patches of
+// octaves whose radii exceed the unrolled ones read them: sift_exact.h).
+template <int RW, bool L64>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE))) void k_gauss_rwp(const Pyramid P, const GaussLaunch L) {
+  using G = RwGeom<RW>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const Octave& oc = P.oct[L.o];
+  int lb = blockIdx.x;
+  const int bpi = L.gx * L.gy * L.G;
+  if (L.xcd_band) {
+    const int nb = bpi * L.nimg, q = nb >> 3, rm = nb & 7, xc = lb & 7;
+    lb = xc * q + min(xc, rm) + (lb >> 3);
+  }
+  const int im = lb / bpi;
+  lb -= im * bpi;
+  float* const L_gauss = L.gauss ? L.gauss + im * L.gauss_bs : nullptr;
+  float* const L_dog = L.dog + im * L.dog_bs;
+  double* const L_next_seed = L.next_seed ? L.next_seed + im * L.seed_bs : nullptr;
+  double* const L_l64 = L64 ? L.l64 + im * L.l64_bs : nullptr;
+  const double* const L_base = L.base + im * L.base_bs;
+  const int bz = lb % L.G, bt = lb / L.G;
+  const int bx = bt % L.gx, by = bt / L.gx + L.by0;
+  const int h = oc.h, w = oc.w, w8 = w * 8;
+  const int x0 = bx * G::TW, y0 = by * kRwRows;
+  const int c = threadIdx.x;  // strip column
+  const __amdgpu_buffer_rsrc_t brs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
+  const int bxoff = clampi(x0 - RW + c, 0, w - 1) * 8;
+  if constexpr (RW > 24) {  // zero the strip columns past 255 (read by rwp_horz_gen's last steps)
+    constexpr int GAP = 14;  // doubles from a row's column 256 to the next row (<= 14)
+    const int b = c / (8 * GAP), t = (c / GAP) & 7, j = c % GAP;
+    const int a = rw_row(t) + 256 + j, end = t < 7 ? rw_row(t + 1) : kRwStrip;
+    if (b < 2 && a < end) smem[b * kRwStrip + a] = 0.0;
+  }
+  // Horizontal items as in k_gauss_rw; lanes without an item read item NCG - 1 and store nothing.
+  int hcg, hr0, hr1;
+  {
+    int g, j;
+    b128_group(c & 63, g, j);
+    const int gid = 4 * (c >> 6) + g;
+    hcg = 8 * (gid >> 1) + (j & 7);
+    hr0 = j < 8 ? (gid & 1) : 6 + (gid & 1);
+    hr1 = j < 8 ? 4 + (gid & 1) : 2 + (gid & 1);
+  }
+  const bool hact = hcg < G::NCG;
+  if (!hact) hcg = G::NCG - 1;
+  const long long plane = (long long)h * w;
+  const unsigned pb = (unsigned)plane * 4u;
+  const unsigned sbytes = L_next_seed ? (unsigned)((h + 1) / 2) * (unsigned)L.next_w * 8u : 0u;
+  int voff[2], soff[2], loff[2];
+  {
+    const int x = x0 + 4 * hcg;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int y = y0 + (i ? hr1 : hr0);
+      const bool own = hact && y < h && x < w;
+      voff[i] = own ? (y * w + x) * 4 : 0x7ffffff0;
+      loff[i] = own ? (y * w + x) * 8 : 0x7fffffe0;
+      soff[i] = own && !(y & 1) ? ((y >> 1) * L.next_w + (x >> 1)) * 8 : 0x7ffffff0;
+    }
+  }
+  const int s_begin = L.gb[bz], s_end = L.gb[bz + 1];
+  const int s_first = max(0, s_begin - 1);
+  const bool st = !(L.dbg & 1);  // dbg 1: timing without plane stores
+  double lprev[2][4];
+  double va[8], vb[8];
+  constexpr int NCH = (2 * RW + 15) >> 3;  // chunks of the widest window
+  rwp_load(brs, bxoff, y0 - oc.rad[s_first], h, w8, va);
+  {
+    // Six empty stores (a zero-size descriptor the compiler cannot see is
+    // empty) after the first chunk's loads: the loop is entered with the
+    // same vector-memory queue as every scale leaves it (next chunk, then
+    // the scale's six stores), so the waitcnt pass's merge at the loop head
+    // waits only for the loads (vmcnt(6)), not for everything.
+    const __amdgpu_buffer_rsrc_t rz =
+        __builtin_amdgcn_make_buffer_rsrc(L_dog, 0, (unsigned)L.dbg & 0x40000000u, 0x00020000);
+    const double zz[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bstore4(rz, 16 * i, zz);
+#pragma unroll
+    for (int i = 0; i < (L64 ? 6 : 2); ++i) bstore_f64x2(rz, 64 + 16 * i, 0.0, 0.0);
+  }
+  bool nb = false;  // this scale's first chunk is in vb
+  for (int s = s_first; s < s_end; ++s) {
+    const cdouble* wp = (const cdouble*)(P.wts + oc.wofs[s]);
+    const int r = oc.rad[s];
+    const int nch = (2 * r + 15) >> 3;  // ceil((2r + 8) / 8)
+    const int rnext = y0 - oc.rad[min(s + 1, s_end - 1)];  // (the last scale's is never used)
+    const int rb = y0 - r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) va[k] = nb ? vb[k] : va[k];
+    double acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+    // Chunk positions unrolled (uniform guards): chunk j is in va for even j,
+    // vb for odd j; position j issues chunk j + 1 (or the next scale's first
+    // chunk) into the other buffer before its fmas.
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      if (j < nch) {
+        const int rl = j + 1 < nch ? rb + 8 * (j + 1) : rnext;
+        if (j & 1) {
+          rwp_load(brs, bxoff, rl, h, w8, va);
+          rwp_fma<false>(wp + 8 * j, vb, acc);
+        } else {
+          rwp_load(brs, bxoff, rl, h, w8, vb);
+          if (j == 0) rwp_fma<true>(wp, va, acc);
+          else rwp_fma<false>(wp + 8 * j, va, acc);
+        }
+      }
+    }
+    nb = nch & 1;
+    double* Vs = smem + (s & 1) * kRwStrip;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) Vs[rw_row(t) + c] = acc[t];
+    lds_barrier();
+    int hc = hcg, h0 = hr0, h1 = hr1;
+    asm volatile("" : "+v"(hc), "+v"(h0), "+v"(h1));  // per-scale opaque: no hoisted per-radius addresses
+    double o[2][4];
+    constexpr int RU = RW < 24 ? RW : 24;  // unrolled radii
+    if (RW <= 24 || r <= RU)
+      rw_horz_any_<RW>(std::make_integer_sequence<int, RU + 1>{}, r, Vs + rw_row(h0) + 4 * hc,
+                       Vs + rw_row(h1) + 4 * hc, wp, o);
+    else
+      rwp_horz_gen<RW>(Vs + rw_row(h0) + 4 * hc, Vs + rw_row(h1) + 4 * hc, r, wp, o);
+    const bool sto = s >= s_begin && st;
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L_gauss ? L_gauss + s * plane : L_dog, 0,
+                                                                         sto && L_gauss ? pb : 0u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L_dog + (s > 0 ? s - 1 : 0) * plane, 0,
+                                                                         sto && s > 0 ? pb : 0u, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      double d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = lprev[i][q] - o[i][q];
+      bstore4(rg, voff[i], o[i]);
+      bstore4(rd, voff[i], d);
+    }
+    {  // the next octave's base: L_S at even rows and columns (dropped at every other scale)
+      const __amdgpu_buffer_rsrc_t rsd =
+          __builtin_amdgcn_make_buffer_rsrc(L_next_seed ? (void*)L_next_seed : (void*)L_dog, 0,
+                                            s == P.S && s >= s_begin ? sbytes : 0u, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) bstore_f64x2(rsd, soff[i], o[i][0], o[i][2]);
+    }
+    if constexpr (L64) {  // fp64 plane s for the exact passes
+      const __amdgpu_buffer_rsrc_t rl =
+          __builtin_amdgcn_make_buffer_rsrc(L_l64 + s * plane, 0, sto ? (unsigned)plane * 8u : 0u, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        bstore_f64x2(rl, loff[i], o[i][0], o[i][1]);
+        bstore_f64x2(rl, loff[i] + 16, o[i][2], o[i][3]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lprev[i][q] = o[i][q];
+  }
+}
+
 // Octaves >= 1 through k_gauss_rw: radii up to SIFT_RW_R (the register
 // window of 8 + 2 RW rows per lane; default 12: octave 1 at 4K and 1080p,
 // 0.172 -> 0.158 ms at 4K; RW 24 for octave 2 measured slower, 0.097 ->
@@ -1535,7 +1792,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
 // columns (SIFT_RW=0: k_gauss_dog, A/B builds).
 static int rw_width(const Pyramid& P, int o) {
   const int R = P.oct[o].rmax;
-  return R <= 12 ? 12 : R <= 16 ? 16 : R <= 24 ? 24 : 0;
+  return R <= 12 ? 12 : R <= 16 ? 16 : R <= 24 ? 24 : R <= 48 ? 48 : 0;
+}
+
+// The pipelined streamed kernel (k_gauss_rwp) issues the same 16-byte buffer
+// stores at every scale, so it needs every plane it writes 16-byte aligned:
+// octave width a multiple of 4, plane offsets (and a batch's per-image
+// strides) multiples of 16 bytes, the next octave's base likewise.
+static bool rwp_ok(const Pyramid& P, int o) {
+  static const int on = exp_knob("SIFT_RWP", 0);
+  const Octave& oc = P.oct[o];
+  if (!on || o < 1 || (oc.w & 3) || 8.0 * oc.h * oc.w >= 2147483648.0) return false;
+  if ((oc.dog_off & 3) || (oc.gauss_off & 3)) return false;
+  if (o + 1 < P.O && (P.oct[o + 1].seed_off & 1)) return false;
+  if (P.nimg > 1) {
+    const long long tot = P.ND > 0 ? P.dog_bstride / P.ND : 0;
+    if ((P.dog_bstride & 3) || ((tot * P.NS) & 3) || (P.seed_bstride & 1)) return false;
+  }
+  return true;
+}
+
+// Octaves whose radii exceed the unrolled ones (25..48: 4K / 1080p octave 3,
+// 8K octave 3) run k_gauss_rwp<48> -- one launch, 160-column tiles, the
+// split pass's scratch round trip gone -- and keep their fp64 planes for the
+// exact passes (the split pass's vertical sums served them before).
+static bool rwp_big(const Pyramid& P, int o) {
+  static const int on = exp_knob("SIFT_RWP_BIG", 0);
+  const int r = P.oct[o].rmax;
+  return on && r > 24 && r <= 48 && P.oct[o].w >= 2 && rwp_ok(P, o);
 }
 
 // Octaves >= 1 whose radii exceed the register window (SIFT_RW_R) up to 24
@@ -1543,12 +1827,13 @@ static int rw_width(const Pyramid& P, int o) {
 // tiles in a 256-column strip instead of k_gauss_dog's 64-column tiles with
 // (64 + 2r) / 64 of the vertical work (SIFT_RWS=0: k_gauss_dog, A/B builds).
 // SIFT_RWS bit 0: radii 13..24; bit 1: also the register-window octaves
-// (radii <= 12) streamed.
+// (radii <= 12) streamed.  Radii 25..48: rwp_big.
 static bool gauss_rws(const Pyramid& P, int o) {
   static const int on = exp_knob("SIFT_RWS", SIFT_RWS_DEFAULT);
   static const int rlim = exp_knob("SIFT_RW_R", 12);
   const int r = P.oct[o].rmax;
-  if (!on || o < 1 || P.oct[o].w < 2 || r > 24 || gauss_keep_l64(P, o)) return false;
+  if (o >= 1 && r > 24) return rwp_big(P, o);
+  if (!on || o < 1 || P.oct[o].w < 2 || gauss_keep_l64(P, o)) return false;
   return r > std::min(rlim, 24) ? (on & 1) != 0 : (on & 2) != 0;
 }
 
@@ -1560,7 +1845,17 @@ bool gauss_wide(const Pyramid& P, int o) {
          gauss_rws(P, o);
 }
 
-static int rw_tile_w(const Pyramid& P, int o) { return rw_width(P, o) <= 16 ? 224 : 192; }
+// k_gauss_rwp for a streamed octave (its launch: the pointers as well).
+static bool gauss_rwp(const Pyramid& P, const GaussLaunch& L) {
+  const bool seed_ok = !L.next_seed || ((L.next_w & 1) == 0 && !(reinterpret_cast<uintptr_t>(L.next_seed) & 15));
+  const bool l64_ok = !L.l64 || !(reinterpret_cast<uintptr_t>(L.l64) & 15);
+  return rwp_ok(P, L.o) && L.vec && seed_ok && l64_ok;
+}
+
+static int rw_tile_w(const Pyramid& P, int o) {
+  const int RW = rw_width(P, o);
+  return RW <= 16 ? 224 : RW <= 24 ? 192 : 160;
+}
 static size_t rw_lds(const Pyramid& P, int o) { (void)P; (void)o; return sizeof(double) * 2 * kRwStrip; }
 
 // Materialised octave-0 base (fp64), for octave-0 radii beyond kUR.
@@ -1592,7 +1887,7 @@ bool gauss_needs_base0(const Pyramid& P) { return P.oct[0].rmax > kUR; }
 // S=5: octaves 4 and 5; at 4K octave 3, radius 47, it measured slower: 0.71 -> 0.74 ms pass).
 bool gauss_keep_l64(const Pyramid& P, int o) {
   static const int rmin = exp_knob("SIFT_L64_R", 90);
-  return o >= 1 && rmin > 0 && P.oct[o].rmax >= rmin;
+  return o >= 1 && ((rmin > 0 && P.oct[o].rmax >= rmin) || rwp_big(P, o));
 }
 
 // Octaves o >= 1 whose largest radius reaches SIFT_VSPLIT_R (default 40; 0 =
@@ -1867,7 +2162,14 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     const dim3 grid(L.gx * L.gy * L.G * L.nimg);
     const size_t lds = occupancy_lds(L.o, rw_lds(P, L.o));
     // (the streamed kernels use the tile geometry of their RW, as the window ones)
-    if (gauss_rws(P, L.o) && RW == 12) hipLaunchKernelGGL((k_gauss_rw<12, true>), grid, dim3(256), lds, st, P, L);
+    if (RW == 48) {  // rwp_big: no other kernel for these radii in this geometry
+      if (!gauss_rwp(P, L) || !L.l64) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((k_gauss_rwp<48, true>), grid, dim3(256), lds, st, P, L);
+    } else if (gauss_rws(P, L.o) && gauss_rwp(P, L)) {
+      if (RW == 12) hipLaunchKernelGGL((k_gauss_rwp<12, false>), grid, dim3(256), lds, st, P, L);
+      else if (RW == 16) hipLaunchKernelGGL((k_gauss_rwp<16, false>), grid, dim3(256), lds, st, P, L);
+      else hipLaunchKernelGGL((k_gauss_rwp<24, false>), grid, dim3(256), lds, st, P, L);
+    } else if (gauss_rws(P, L.o) && RW == 12) hipLaunchKernelGGL((k_gauss_rw<12, true>), grid, dim3(256), lds, st, P, L);
     else if (gauss_rws(P, L.o) && RW == 16) hipLaunchKernelGGL((k_gauss_rw<16, true>), grid, dim3(256), lds, st, P, L);
     else if (gauss_rws(P, L.o)) hipLaunchKernelGGL((k_gauss_rw<24, true>), grid, dim3(256), lds, st, P, L);
     else if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
