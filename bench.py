@@ -436,6 +436,7 @@ def main():
             iso[k] += t[k] / n_iso
         for o, v in enumerate(ctx.octave_timings()):
             iso_oct[o] += v / n_iso
+    pass_kernels = ctx.pass_kernels()  # the library's own record of the launches (sift_last_pass_kernels)
     with sift_amd.Context(dev) as vctx:
         if batched:  # the batch against the same images detected one by one
             ref = []
@@ -516,9 +517,8 @@ def main():
                                "context" % nin)),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "Gaussian+DoG pass: every launch of one image's %d octaves%s (4K O4 S5: k_gauss_dog for "
-                          "octaves 0 and 2, k_gauss_rw for octave 1, k_gauss_vert + k_gauss_dog for octave 3)" %
-                          (O, ", each over the batch of %d images" % Bt if batched else ""),
+                "kernel": "Gaussian+DoG pass: every launch of one image's %d octaves%s (%s)" %
+                          (O, ", each over the batch of %d images" % Bt if batched else "", pass_kernels),
                 "achieved": round(gbs(B, iso_pass), 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SIFT_ABI_VERSION 8
+#define SIFT_ABI_VERSION 9
 
 /* Opaque context (one HIP stream + device-resident pyramids). */
 struct sift_ctx;
@@ -291,6 +291,13 @@ int sift_last_timings(struct sift_ctx *ctx, sift_timings *t);
  * Launch o is timed from the end of launch o-1 on the same stream, so with
  * other streams' work overlapping it includes the wait for CUs. */
 int sift_last_octave_timings(struct sift_ctx *ctx, double *ms, int cap, int *n_octaves);
+
+/* The kernels the last build / detection launched for its Gaussian+DoG pass
+ * (ABI version >= 9), one entry per octave: "o0: k_gauss_dog<octave0>; o1:
+ * k_gauss_rw<12>; ..." -- what bench.py's roofline.kernel reports.  Writes
+ * at most cap bytes including the terminating NUL; *len = the full length
+ * (excluding the NUL); SIFT_E_CAPACITY when cap is too small. */
+int sift_last_pass_kernels(struct sift_ctx *ctx, char *buf, size_t cap, size_t *len);
 
 /* Device-to-device copy of the last keypoints into caller device memory
  * (e.g. an RCCL all-gather send buffer), ordered on ctx's stream and

@@ -228,6 +228,7 @@ struct sift_ctx {
   hipEvent_t ev_go[kMaxOctaves]{}; // after octave o's Gaussian+DoG launch (per-octave timings)
   sift_timings tm{};
   std::vector<double> oct_ms;      // per-octave Gaussian+DoG launch time of the last build
+  std::vector<std::string> pass_kn; // per-octave pass kernels of the last build (sift_last_pass_kernels)
 };
 
 #define HIPCHK(call)                                                                        \
@@ -714,10 +715,12 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     ctx->xseed_w = (P.oct[P.O - 1].w + 1) / 2;
     HIPCHK(ctx->xseed.ensure((size_t)ctx->xseed_h * ctx->xseed_w * sizeof(double)));
   }
+  ctx->pass_kn.assign(P.O, std::string());
   for (int o = o_first; o < P.O; ++o) {
     const Octave& oc = P.oct[o];
     hipStream_t ost = ctx->stream;
     if (o < so_end) {
+      ctx->pass_kn[o] = "k_seed_vert + k_seed_horz (next base only)";
       HIPCHK(launch_seed_only(P, o, ctx->seeds.as<double>() + oc.seed_off, ctx->seedv.as<double>(),
                               ctx->seeds.as<double>() + P.oct[o + 1].seed_off, ctx->stream));
       if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ctx->stream));
@@ -753,7 +756,9 @@ static int build_common(sift_ctx* ctx, const float* img_host, const float* img_d
     L.base_bs = o == 0 ? 0 : seeds_pi;
     L.l64_bs = P.l64_bstride;
     L.vsplit_bs = ctx->vsplit_pi;
-    HIPCHK(launch_gauss_dog(P, L, ost));
+    const char* kn = nullptr;
+    HIPCHK(launch_gauss_dog(P, L, ost, 0, -1, &kn));
+    ctx->pass_kn[o] = std::string(o == 0 && base0 ? "k_upsample_base + " : "") + (kn ? kn : "?");
     if (o == o_first) HIPCHK(hipEventRecord(ctx->ev[7], ost));
     HIPCHK(hipEventRecord(ctx->ev_go[o], ost));
   }
@@ -1777,6 +1782,21 @@ int sift_last_octave_timings(sift_ctx* ctx, double* ms, int cap, int* n_out) {
   if (!ms) return SIFT_OK;
   if (cap < n) return set_err(ctx, SIFT_E_CAPACITY, "destination too small (one per octave)");
   for (int o = 0; o < n; ++o) ms[o] = ctx->oct_ms[o];
+  return SIFT_OK;
+}
+
+int sift_last_pass_kernels(sift_ctx* ctx, char* buf, size_t cap, size_t* len) {
+  if (!ctx) return SIFT_E_ARG;
+  std::string t;
+  for (size_t o = 0; o < ctx->pass_kn.size(); ++o) {
+    if (ctx->pass_kn[o].empty()) continue;
+    if (!t.empty()) t += "; ";
+    t += "o" + std::to_string(o) + ": " + ctx->pass_kn[o];
+  }
+  if (len) *len = t.size();
+  if (!buf) return SIFT_OK;
+  if (cap < t.size() + 1) return set_err(ctx, SIFT_E_CAPACITY, "destination too small");
+  std::memcpy(buf, t.c_str(), t.size() + 1);
   return SIFT_OK;
 }
 

@@ -2123,7 +2123,10 @@ static size_t occupancy_lds(int o, size_t lds) {
   return std::max(lds, cap);
 }
 
-hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin, int ty_end) {
+hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin, int ty_end,
+                            const char** kname) {
+  const char* kn_dummy = nullptr;
+  const char*& kn = kname ? *kname : kn_dummy;
   static_assert(kGY == kGaussTileRows, "tile rows");
   const Octave& oc = P.oct[L.o];
   if (L.nimg < 1) L.nimg = 1;
@@ -2165,16 +2168,23 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     if (RW == 48) {  // rwp_big: no other kernel for these radii in this geometry
       if (!gauss_rwp(P, L) || !L.l64) return hipErrorInvalidValue;
       hipLaunchKernelGGL((k_gauss_rwp<48, true>), grid, dim3(256), lds, st, P, L);
+      kn = "k_gauss_rwp<48,l64>";
     } else if (gauss_rws(P, L.o) && gauss_rwp(P, L)) {
       if (RW == 12) hipLaunchKernelGGL((k_gauss_rwp<12, false>), grid, dim3(256), lds, st, P, L);
       else if (RW == 16) hipLaunchKernelGGL((k_gauss_rwp<16, false>), grid, dim3(256), lds, st, P, L);
       else hipLaunchKernelGGL((k_gauss_rwp<24, false>), grid, dim3(256), lds, st, P, L);
-    } else if (gauss_rws(P, L.o) && RW == 12) hipLaunchKernelGGL((k_gauss_rw<12, true>), grid, dim3(256), lds, st, P, L);
-    else if (gauss_rws(P, L.o) && RW == 16) hipLaunchKernelGGL((k_gauss_rw<16, true>), grid, dim3(256), lds, st, P, L);
-    else if (gauss_rws(P, L.o)) hipLaunchKernelGGL((k_gauss_rw<24, true>), grid, dim3(256), lds, st, P, L);
-    else if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
-    else if (RW == 16) hipLaunchKernelGGL(k_gauss_rw<16>, grid, dim3(256), lds, st, P, L);
-    else hipLaunchKernelGGL(k_gauss_rw<24>, grid, dim3(256), lds, st, P, L);
+      kn = RW == 12 ? "k_gauss_rwp<12>" : RW == 16 ? "k_gauss_rwp<16>" : "k_gauss_rwp<24>";
+    } else if (gauss_rws(P, L.o)) {
+      if (RW == 12) hipLaunchKernelGGL((k_gauss_rw<12, true>), grid, dim3(256), lds, st, P, L);
+      else if (RW == 16) hipLaunchKernelGGL((k_gauss_rw<16, true>), grid, dim3(256), lds, st, P, L);
+      else hipLaunchKernelGGL((k_gauss_rw<24, true>), grid, dim3(256), lds, st, P, L);
+      kn = RW == 12 ? "k_gauss_rw<12,true>" : RW == 16 ? "k_gauss_rw<16,true>" : "k_gauss_rw<24,true>";
+    } else {
+      if (RW == 12) hipLaunchKernelGGL(k_gauss_rw<12>, grid, dim3(256), lds, st, P, L);
+      else if (RW == 16) hipLaunchKernelGGL(k_gauss_rw<16>, grid, dim3(256), lds, st, P, L);
+      else hipLaunchKernelGGL(k_gauss_rw<24>, grid, dim3(256), lds, st, P, L);
+      kn = RW == 12 ? "k_gauss_rw<12>" : RW == 16 ? "k_gauss_rw<16>" : "k_gauss_rw<24>";
+    }
     return hipGetLastError();
   }
   const int G = scale_groups(P, L.o);
@@ -2225,14 +2235,19 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
   if (L.fuse) {  // staged octave 0 (gauss_can_fuse)
     if (L.sw == kSW0) hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, true>), grid, dim3(256), lds, st, P, L);
     else hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, true>), grid, dim3(256), lds, st, P, L);
+    kn = "k_gauss_dog<octave0,fused extrema>";
   } else if (tw == 96) {
     hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR96, false, 96>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
+    kn = "k_gauss_dog<96>";
   } else if (staged0(P, L.o) && L.sw == kSW0) {
     hipLaunchKernelGGL((k_gauss_dog<true, kSW0, 8, false>), grid, dim3(256), lds, st, P, L);
+    kn = "k_gauss_dog<octave0>";
   } else if (staged0(P, L.o)) {
     hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, false>), grid, dim3(256), lds, st, P, L);
+    kn = "k_gauss_dog<octave0>";
   } else {
     hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
+    kn = L.vsplit ? "k_gauss_vert + k_gauss_dog<64>" : L.o == 0 ? "k_gauss_dog<octave0,fp64 base>" : "k_gauss_dog<64>";
   }
   return hipGetLastError();
 }

@@ -261,7 +261,10 @@ size_t seed_only_scratch(const Pyramid& P, int o);
 hipError_t launch_seed_only(const Pyramid& P, int o, const double* base, double* vrow, double* next, hipStream_t st);
 // ty_end >= 0: only tile rows [ty_begin, ty_end) of the octave (a band;
 // not for fused or split-pass octaves).
-hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin = 0, int ty_end = -1);
+// kname (optional): the launches this call made, e.g. "k_gauss_rw<12>" or
+// "k_gauss_vert + k_gauss_dog<64>" (a static string; sift_last_pass_kernels).
+hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int ty_begin = 0, int ty_end = -1,
+                            const char** kname = nullptr);
 int gauss_tile_rows(const Pyramid& P, int o);  // tile rows of octave o's Gaussian launch
 constexpr int kGaussTileRows = 32;             // output rows per tile row
 // Tile columns of a fused launch over a w-column octave (= bitmap words per row).

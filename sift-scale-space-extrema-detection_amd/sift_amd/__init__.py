@@ -55,6 +55,7 @@ ABI_SYMBOLS = (
     "sift_rgba_to_gray", "sift_rgba_to_gray_device", "sift_build_scale_space_rgba", "sift_detect_rgba",
     "sift_plane_image", "sift_plane_image_device", "sift_detect_begin_async", "sift_detect_end_async",
     "sift_copy_keypoint_origins_device", "sift_copy_next_seed_device", "sift_last_octave_timings",
+    "sift_last_pass_kernels",
     "sift_detect_from_seed_range_device", "sift_merge_keypoint_blocks_device", "sift_set_owned_rows",
     "sift_last_block_counts", "sift_copy_low_contrast", "sift_set_flags",
     "sift_detect_batch_device", "sift_detect_batch_device_async", "sift_detect_batch",
@@ -167,6 +168,7 @@ def lib():
         "sift_last_counts": (ctypes.c_int, [vp, szp, szp, szp, szp, szp]),
         "sift_last_timings": (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
         "sift_last_octave_timings": (ctypes.c_int, [vp, dp, ctypes.c_int, ip]),
+        "sift_last_pass_kernels": (ctypes.c_int, [vp, ctypes.c_char_p, sz, szp]),
         "sift_detect_from_seed_range_device": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int,
                                                               ctypes.c_int, pp, vp, sz, szp]),
         "sift_merge_keypoint_blocks_device": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_int64), ctypes.c_int,
@@ -661,6 +663,15 @@ class Context:
         self._check(self._L.sift_last_octave_timings(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                                      out.shape[0], ctypes.byref(n)), "sift_last_octave_timings")
         return [float(v) for v in out[:n.value]]
+
+    def pass_kernels(self):
+        """The Gaussian+DoG kernels of the last build / detection, per octave
+        ("o0: k_gauss_dog<octave0>; o1: ...")."""
+        n = ctypes.c_size_t()
+        self._check(self._L.sift_last_pass_kernels(self._h, None, 0, ctypes.byref(n)), "sift_last_pass_kernels")
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._check(self._L.sift_last_pass_kernels(self._h, buf, n.value + 1, ctypes.byref(n)), "sift_last_pass_kernels")
+        return buf.value.decode()
 
     def stream(self):
         return self._L.sift_stream(self._h)

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_defaults():
     L = sift_amd.lib()
-    assert L.sift_abi_version() == 8
+    assert L.sift_abi_version() == 9
     p = sift_amd.Params()
     assert L.sift_params_default(ctypes.byref(p)) == 0
     # src/worker.js:33-37,88

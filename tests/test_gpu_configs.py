@@ -159,6 +159,22 @@ def test_planes_bit_exact_in_gpu_order(gpu_ctx, W, H, O, S, seed):
             np.testing.assert_array_equal(gpu_ctx.plane(sift_amd.PLANE_DOG, o, s), r.dog[o][s].astype(np.float32))
 
 
+@pytest.mark.timeout(300)
+def test_pass_kernels_record(gpu_ctx):
+    """sift_last_pass_kernels names each octave's launches (bench.py's
+    roofline.kernel): 1080p O4 S5 runs octave 0's staged tile kernel, octave 1
+    (radii <= 12) the register-window kernel, octave 2 (radii <= 24) the
+    streamed one and octave 3 (radius 47) the split vertical pass + tiles."""
+    p = sift_amd.make_params(4, 5)
+    gpu_ctx.build_scale_space(blob_image(1920, 1080, seed=3), p)
+    parts = dict(e.split(": ", 1) for e in gpu_ctx.pass_kernels().split("; "))
+    assert sorted(parts) == ["o0", "o1", "o2", "o3"], parts
+    assert parts["o0"].startswith("k_gauss_dog<octave0"), parts
+    assert parts["o1"] == "k_gauss_rw<12>", parts
+    assert parts["o2"] == "k_gauss_rw<24,true>", parts
+    assert parts["o3"] == "k_gauss_vert + k_gauss_dog<64>", parts
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("W,H,O,S,seed", [(3840, 2160, 4, 5, 42), (333, 517, 4, 3, 4), (64, 48, 3, 3, 5)])
 def test_fused_extrema_flag_same_results(gpu_ctx, W, H, O, S, seed):
