@@ -574,8 +574,12 @@ hipError_t launch_band_fill(const Pyramid& P, const BandOrder& B, hipStream_t st
 
 hipError_t launch_refine_fast(const Pyramid& P, const RefineLaunch& R, hipStream_t st) {
   if (R.cap <= 0) return hipSuccess;
-  if (R.exact_planes) hipLaunchKernelGGL(k_refine_fast<true>, dim3((R.cap + 255) / 256), dim3(256), 0, st, P, R);
-  else hipLaunchKernelGGL(k_refine_fast<false>, dim3((R.cap + 255) / 256), dim3(256), 0, st, P, R);
+  // SIFT_REFINE_LDS (experiments): dynamic LDS bytes per block, to cap the
+  // blocks per CU (the candidates in flight, i.e. the DoG lines an XCD's L2
+  // must hold at once).
+  static const int lds = exp_knob("SIFT_REFINE_LDS", 0);
+  if (R.exact_planes) hipLaunchKernelGGL(k_refine_fast<true>, dim3((R.cap + 255) / 256), dim3(256), lds, st, P, R);
+  else hipLaunchKernelGGL(k_refine_fast<false>, dim3((R.cap + 255) / 256), dim3(256), lds, st, P, R);
   return hipGetLastError();
 }
 
