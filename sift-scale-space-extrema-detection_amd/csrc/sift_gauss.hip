@@ -163,6 +163,19 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Buffer descriptor of a wave-uniform pointer, the pointer's halves taken
+// through readfirstlane: a per-scale plane offset the compiler computed in
+// VGPRs (s * plane as a 64-bit VALU product) otherwise makes the descriptor
+// divergent and every store through it a waterfall loop (4 readfirstlanes,
+// compares and an exec loop per store instruction; r6 ISA of k_gauss_rw).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t urs(const void* p, unsigned bytes) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  void* q = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 __device__ __forceinline__ double load_f64(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
 }
@@ -506,8 +519,7 @@ __global__ __launch_bounds__(256) void k_gauss_vert(const Pyramid P, int o, cons
   const int x = blockIdx.x * kGX + lane;
   const int y0 = blockIdx.y * kVertRows + kVertNO * wv;
   if (y0 >= h) return;  // wave-uniform
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, h * w * 8,
-                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = urs(const_cast<double*>(base), h * w * 8);
   const int xoff = min(x, w - 1) * 8;
   const int NJ = 2 * r + kVertNO, yb = y0 - r;
   double acc[kVertNO];
@@ -812,11 +824,52 @@ __device__ __forceinline__ void horz_o0(const GTile& T, const cdouble* wp, const
 }
 
 // ---------------------------------------------------------------------------
-// Radius dispatch (uniform branch).
+// Radius dispatch (uniform branch): a binary search over the unrolled radii
+// LO..HI (log2 compares and branches per dispatch instead of a compare chain
+// of up to HI; every scale of every block dispatches twice).
 // ---------------------------------------------------------------------------
+template <int LO, int HI, class F>
+__device__ __forceinline__ void rdispatch(int r, F&& f) {
+  if constexpr (LO == HI) {
+    f(std::integral_constant<int, LO>{});
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (r <= MID) rdispatch<LO, MID>(r, f);
+    else rdispatch<MID + 1, HI>(r, f);
+  }
+}
+
+#ifndef SIFT_BIN_STREAM
+#define SIFT_BIN_STREAM 1  // binary radius dispatch in the streamed k_gauss_rw<RW, true> too
+#endif
+#ifndef SIFT_BIN_TILE
+#define SIFT_BIN_TILE 1  // binary radius dispatch in the k_gauss_dog tile kernels of octaves >= 1
+#endif
+#ifndef SIFT_BIN_OCT0
+#define SIFT_BIN_OCT0 0  // ... and in octave 0's
+#endif
+// Measured (r6f / r6g, profiles/r6g_radius_dispatch_ab.txt): 4K octave 1
+// (register window) 0.162 -> 0.149 ms, octave 2 (streamed) 0.095 -> 0.089 ms,
+// octave 3's tiles -2 us; octave 0 keeps the compare chain (the binary form
+// takes it from 92 to 105 VGPRs, 5 -> 4 waves per SIMD: 0.364 -> 0.383 ms;
+// bounded to 96 it spills: 0.370 ms).
 template <bool OCT0, int... Rs>
 __device__ __forceinline__ void vert_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
                                          const cdouble* wp, double* V) {
+  constexpr int N = sizeof...(Rs) - 1;
+  if constexpr (OCT0 ? SIFT_BIN_OCT0 : SIFT_BIN_TILE) {
+    if constexpr (OCT0) {
+      rdispatch<0, N>(r, [&](auto R) { vert_o0<decltype(R)::value>(T, wp, V); });
+    } else if (r <= N) {
+      if (kVert2 && T.w >= 2) rdispatch<0, N>(r, [&](auto R) { vert_glob2<decltype(R)::value>(T, wp, V); });
+      else rdispatch<0, N>(r, [&](auto R) { vert_glob<decltype(R)::value>(T, wp, V); });
+    } else if (kVert2 && kVertGen2 && T.w >= 2 && r <= 32) {
+      vert_glob_gen2(T, r, wp, V);
+    } else {
+      vert_glob_gen(T, r, wp, V);
+    }
+    return;
+  }
   bool done = false;
   if constexpr (OCT0) {
     ((!done && r == Rs ? (vert_o0<Rs>(T, wp, V), done = true) : false), ...);
@@ -834,6 +887,17 @@ __device__ __forceinline__ void vert_any_(std::integer_sequence<int, Rs...>, con
 template <bool OCT0, int... Rs>
 __device__ __forceinline__ void horz_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
                                          const cdouble* wp, const double* V, double (&out)[kNR][4]) {
+  constexpr int N = sizeof...(Rs) - 1;
+  if constexpr (OCT0 ? SIFT_BIN_OCT0 : SIFT_BIN_TILE) {
+    if constexpr (OCT0) {
+      rdispatch<0, N>(r, [&](auto R) { horz_o0<decltype(R)::value>(T, wp, V, out); });
+    } else if (r <= N) {
+      rdispatch<0, N>(r, [&](auto R) { horz_full<decltype(R)::value>(T, wp, V, out); });
+    } else {
+      horz_full_gen(T, r, wp, V, out);
+    }
+    return;
+  }
   bool done = false;
   if constexpr (OCT0) {
     ((!done && r == Rs ? (horz_o0<Rs>(T, wp, V, out), done = true) : false), ...);
@@ -846,12 +910,20 @@ __device__ __forceinline__ void horz_any_(std::integer_sequence<int, Rs...>, con
 template <int... Rs>
 __device__ __forceinline__ void vert96_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
                                            const cdouble* wp, double* V) {
+  if constexpr (SIFT_BIN_TILE) {
+    rdispatch<0, sizeof...(Rs) - 1>(r, [&](auto R) { vert_glob2<decltype(R)::value, 96>(T, wp, V); });
+    return;
+  }
   bool done = false;
   ((!done && r == Rs ? (vert_glob2<Rs, 96>(T, wp, V), done = true) : false), ...);
 }
 template <int... Rs>
 __device__ __forceinline__ void horz96_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
                                            const cdouble* wp, const double* V, double (&out)[3][4]) {
+  if constexpr (SIFT_BIN_TILE) {
+    rdispatch<0, sizeof...(Rs) - 1>(r, [&](auto R) { horz_full96<decltype(R)::value>(T, wp, V, out); });
+    return;
+  }
   bool done = false;
   ((!done && r == Rs ? (horz_full96<Rs>(T, wp, V, out), done = true) : false), ...);
 }
@@ -859,6 +931,10 @@ __device__ __forceinline__ void horz96_any_(std::integer_sequence<int, Rs...>, c
 template <class Epi, int... Rs>
 __device__ __forceinline__ void horz96s_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
                                             const cdouble* wp, const double* V, Epi&& epi) {
+  if constexpr (SIFT_BIN_TILE) {
+    rdispatch<0, sizeof...(Rs) - 1>(r, [&](auto R) { horz_full96_seq<decltype(R)::value>(T, wp, V, epi); });
+    return;
+  }
   bool done = false;
   ((!done && r == Rs ? (horz_full96_seq<Rs>(T, wp, V, epi), done = true) : false), ...);
 }
@@ -973,7 +1049,10 @@ __device__ __forceinline__ void fused_decide(const Pyramid& P, const GaussLaunch
 // horz_full96); NI items of 4 columns x 1 row per lane in the horizontal pass
 // and the epilogue.
 template <bool OCT0, int SWC, int RMAX, bool XF, int TW = kGX>
-__global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1)) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
+#ifndef SIFT_W0
+#define SIFT_W0 1  // octave-0 tile kernel: minimum blocks (= waves) per SIMD the register allocation must allow
+#endif
+__global__ __launch_bounds__(256, OCT0 ? SIFT_W0 : (TW == 96 ? SIFT_W96 : SIFT_MINW1)) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
   static_assert(TW == kGX || (TW == 96 && !OCT0 && !XF && RMAX <= 16), "96-column tiles: octaves >= 1, unrolled radii");
   constexpr int NI = TW == kGX ? kNR : 3;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1035,7 +1114,7 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
   T.sw = SWC > 0 ? SWC : L.sw;
   T.hrm = cl2(oc.rmax);
   if (!OCT0)
-    T.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, T.h * T.w * 8, 0x00020000);
+    T.rsrc = urs(const_cast<double*>(L_base), T.h * T.w * 8);
   // One strip: every wave writes (vertical pass) and reads (horizontal pass)
   // only its own 8 strip rows.
   const int nstrip = kGY * T.sw;
@@ -1110,9 +1189,9 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
       const unsigned pb = (unsigned)plane * 4u;
       const bool stor = s >= s_begin && st;
       const __amdgpu_buffer_rsrc_t rg =
-          __builtin_amdgcn_make_buffer_rsrc(L_gauss ? L_gauss + s * plane : L_dog, 0, pb, 0x00020000);
+          urs(L_gauss ? L_gauss + s * plane : L_dog, pb);
       const __amdgpu_buffer_rsrc_t rd =
-          __builtin_amdgcn_make_buffer_rsrc(L_dog + (s > 0 ? s - 1 : 0) * plane, 0, pb, 0x00020000);
+          urs(L_dog + (s > 0 ? s - 1 : 0) * plane, pb);
       horz96s_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V,
                    [&](int i, const double (&o)[4]) {
                      double d[4];
@@ -1167,12 +1246,12 @@ __global__ __launch_bounds__(256, OCT0 ? 1 : (TW == 96 ? SIFT_W96 : SIFT_MINW1))
       if (L.vec) {
         const unsigned pb = (unsigned)plane * 4u;
         if (L_gauss) {
-          const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000);
+          const __amdgpu_buffer_rsrc_t rg = urs(L_gauss + s * plane, pb);
 #pragma unroll
           for (int i = 0; i < NI; ++i) bstore4(rg, voff[i], out[i]);
         }
         if (s > 0) {
-          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000);
+          const __amdgpu_buffer_rsrc_t rd = urs(L_dog + (s - 1) * plane, pb);
 #pragma unroll
           for (int i = 0; i < NI; ++i) bstore4(rd, voff[i], d[i]);
         }
@@ -1366,30 +1445,20 @@ template <int RW, int... Rs>
 __device__ __forceinline__ void rw_vert_any_(std::integer_sequence<int, Rs...>, int r,
                                             const double (&win)[RwGeom<RW>::NW], const cdouble* wp,
                                             double (&acc)[8]) {
-  bool done = false;
-  ((!done && r == Rs ? (rw_vert<Rs, RW>(win, wp, acc), done = true) : false), ...);
+  rdispatch<0, sizeof...(Rs) - 1>(r, [&](auto R) { rw_vert<decltype(R)::value, RW>(win, wp, acc); });
 }
-template <int RW, int... Rs>
+// BIN: binary dispatch (the register-window kernel); the streamed kernels keep
+// the compare chain (the binary form cost k_gauss_rw<24, true> 82 -> 100 VGPRs).
+template <int RW, bool BIN = true, int... Rs>
 __device__ __forceinline__ void rw_horz_any_(std::integer_sequence<int, Rs...>, int r, const double* ra,
                                             const double* rb, const cdouble* wp, double (&out)[2][4]) {
-  bool done = false;
-  ((!done && r == Rs ? (rw_horz<Rs, RW>(ra, rb, wp, out), done = true) : false), ...);
+  if constexpr (BIN) {
+    rdispatch<0, sizeof...(Rs) - 1>(r, [&](auto R) { rw_horz<decltype(R)::value, RW>(ra, rb, wp, out); });
+  } else {
+    bool done = false;
+    ((!done && r == Rs ? (rw_horz<Rs, RW>(ra, rb, wp, out), done = true) : false), ...);
+  }
 }
-// ... with the epilogue inside each radius variant (no join of the outputs:
-// the variants' accumulators go straight to their stores).
-template <int RW, class Epi, int... Rs>
-__device__ __forceinline__ void rw_horz_epi_(std::integer_sequence<int, Rs...>, int r, const double* ra,
-                                            const double* rb, const cdouble* wp, Epi&& epi) {
-  bool done = false;
-  ((!done && r == Rs ? ([&] {
-     double o[2][4];
-     rw_horz<Rs, RW>(ra, rb, wp, o);
-     epi(o);
-   }(), done = true)
-                     : false),
-   ...);
-}
-
 // Streamed vertical pass of one strip column (k_gauss_rw<RW, true>): the
 // scale's own window rows y0 - r .. y0 + 7 + r loaded per scale from the base
 // plane (L2-resident for the mid-radius octaves: XCD-banded tiles), in
@@ -1439,7 +1508,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
   const int c = threadIdx.x;  // strip column
   // The lane's base window: rows y0 - RW .. y0 + 7 + RW of image column x0 - RW + c (clamped).
   const __amdgpu_buffer_rsrc_t brs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
+      urs(const_cast<double*>(L_base), h * w * 8);
   const int bxoff = clampi(x0 - RW + c, 0, w - 1) * 8;
   double win[STREAM ? 1 : G::NW];
   if constexpr (!STREAM) {
@@ -1492,8 +1561,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
       int hc = hcg, h0 = hr0, h1 = hr1;
       asm volatile("" : "+v"(hc), "+v"(h0), "+v"(h1));  // per-scale opaque: no hoisted per-radius addresses
       double o[2][4];
-      rw_horz_any_<RW>(std::make_integer_sequence<int, RW + 1>{}, r, Vs + rw_row(h0) + 4 * hc,
-                       Vs + rw_row(h1) + 4 * hc, wp, o);
+      rw_horz_any_<RW, !STREAM || SIFT_BIN_STREAM>(std::make_integer_sequence<int, RW + 1>{}, r, Vs + rw_row(h0) + 4 * hc,
+                                Vs + rw_row(h1) + 4 * hc, wp, o);
       const int x = x0 + 4 * hc, nvalid = w - x;
       const unsigned pb = (unsigned)plane * 4u;
 #pragma unroll
@@ -1507,9 +1576,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
           if (L.vec) {
             const int voff = own ? (y * w + x) * 4 : 0x7ffffff0;  // dropped past the plane
             if (L_gauss)
-              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_gauss + s * plane, 0, pb, 0x00020000), voff, o[i]);
+              bstore4(urs(L_gauss + s * plane, pb), voff, o[i]);
             if (s > 0)
-              bstore4(__builtin_amdgcn_make_buffer_rsrc(L_dog + (s - 1) * plane, 0, pb, 0x00020000), voff, d);
+              bstore4(urs(L_dog + (s - 1) * plane, pb), voff, d);
           } else if (own) {
             const long long pp = (long long)y * w + x;
             if (L_gauss) store4(L_gauss + s * plane + pp, o[i], nvalid);
@@ -1650,7 +1719,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
   const int x0 = bx * G::TW, y0 = by * kRwRows;
   const int c = threadIdx.x;  // strip column
   const __amdgpu_buffer_rsrc_t brs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(L_base), 0, h * w * 8, 0x00020000);
+      urs(const_cast<double*>(L_base), h * w * 8);
   const int bxoff = clampi(x0 - RW + c, 0, w - 1) * 8;
   if constexpr (RW > 24) {  // zero the strip columns past 255 (read by rwp_horz_gen's last steps)
     constexpr int GAP = 14;  // doubles from a row's column 256 to the next row (<= 14)
@@ -1699,7 +1768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
     // the scale's six stores), so the waitcnt pass's merge at the loop head
     // waits only for the loads (vmcnt(6)), not for everything.
     const __amdgpu_buffer_rsrc_t rz =
-        __builtin_amdgcn_make_buffer_rsrc(L_dog, 0, (unsigned)L.dbg & 0x40000000u, 0x00020000);
+        urs(L_dog, (unsigned)L.dbg & 0x40000000u);
     const double zz[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int i = 0; i < 4; ++i) bstore4(rz, 16 * i, zz);
@@ -1745,15 +1814,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
     double o[2][4];
     constexpr int RU = RW < 24 ? RW : 24;  // unrolled radii
     if (RW <= 24 || r <= RU)
-      rw_horz_any_<RW>(std::make_integer_sequence<int, RU + 1>{}, r, Vs + rw_row(h0) + 4 * hc,
-                       Vs + rw_row(h1) + 4 * hc, wp, o);
+      rw_horz_any_<RW, false>(std::make_integer_sequence<int, RU + 1>{}, r, Vs + rw_row(h0) + 4 * hc,
+                              Vs + rw_row(h1) + 4 * hc, wp, o);
     else
       rwp_horz_gen<RW>(Vs + rw_row(h0) + 4 * hc, Vs + rw_row(h1) + 4 * hc, r, wp, o);
     const bool sto = s >= s_begin && st;
-    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(L_gauss ? L_gauss + s * plane : L_dog, 0,
-                                                                         sto && L_gauss ? pb : 0u, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(L_dog + (s > 0 ? s - 1 : 0) * plane, 0,
-                                                                         sto && s > 0 ? pb : 0u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rg = urs(L_gauss ? L_gauss + s * plane : L_dog, sto && L_gauss ? pb : 0u);
+    const __amdgpu_buffer_rsrc_t rd = urs(L_dog + (s > 0 ? s - 1 : 0) * plane, sto && s > 0 ? pb : 0u);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       double d[4];
@@ -1764,14 +1831,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_RW_WPE
     }
     {  // the next octave's base: L_S at even rows and columns (dropped at every other scale)
       const __amdgpu_buffer_rsrc_t rsd =
-          __builtin_amdgcn_make_buffer_rsrc(L_next_seed ? (void*)L_next_seed : (void*)L_dog, 0,
-                                            s == P.S && s >= s_begin ? sbytes : 0u, 0x00020000);
+          urs(L_next_seed ? (void*)L_next_seed : (void*)L_dog, s == P.S && s >= s_begin ? sbytes : 0u);
 #pragma unroll
       for (int i = 0; i < 2; ++i) bstore_f64x2(rsd, soff[i], o[i][0], o[i][2]);
     }
     if constexpr (L64) {  // fp64 plane s for the exact passes
       const __amdgpu_buffer_rsrc_t rl =
-          __builtin_amdgcn_make_buffer_rsrc(L_l64 + s * plane, 0, sto ? (unsigned)plane * 8u : 0u, 0x00020000);
+          urs(L_l64 + s * plane, sto ? (unsigned)plane * 8u : 0u);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         bstore_f64x2(rl, loff[i], o[i][0], o[i][1]);
