@@ -1048,10 +1048,20 @@ __device__ __forceinline__ void fused_decide(const Pyramid& P, const GaussLaunch
 // TW: tile width (64; 96 for octaves >= 1 whose radii are all unrolled,
 // horz_full96); NI items of 4 columns x 1 row per lane in the horizontal pass
 // and the epilogue.
-template <bool OCT0, int SWC, int RMAX, bool XF, int TW = kGX>
+#ifndef SIFT_VS_KERNEL
+#define SIFT_VS_KERNEL 1  // split-pass octaves run the VS instance of the tile kernel
+#endif
+#ifndef SIFT_VS_RMAX
+#define SIFT_VS_RMAX 12  // ... with unrolled horizontal radii up to this
+#endif
 #ifndef SIFT_W0
 #define SIFT_W0 1  // octave-0 tile kernel: minimum blocks (= waves) per SIMD the register allocation must allow
 #endif
+// VS: the split-pass instance (octaves with a k_gauss_vert launch): its strips
+// come from the split pass's vertical sums only, so the vertical radius
+// variants are not compiled into it (round 6: the shared instance spilled
+// 126 SGPRs into VGPR lanes, readlane / writelane in every scale).
+template <bool OCT0, int SWC, int RMAX, bool XF, int TW = kGX, bool VS = false>
 __global__ __launch_bounds__(256, OCT0 ? SIFT_W0 : (TW == 96 ? SIFT_W96 : SIFT_MINW1)) void k_gauss_dog(const Pyramid P, const GaussLaunch L) {
   static_assert(TW == kGX || (TW == 96 && !OCT0 && !XF && RMAX <= 16), "96-column tiles: octaves >= 1, unrolled radii");
   constexpr int NI = TW == kGX ? kNR : 3;
@@ -1226,7 +1236,9 @@ __global__ __launch_bounds__(256, OCT0 ? SIFT_W0 : (TW == 96 ? SIFT_W96 : SIFT_M
       wave_lds_fence();  // this wave's strip rows written -> read by its other lanes
       horz96_any_(std::make_integer_sequence<int, RMAX + 1>{}, Ts, oc.rad[s], wp, V, out);
     } else {
-      if constexpr (!OCT0) {
+      if constexpr (VS) {
+        vert_copy(Ts, oc.rad[s], L_vsplit + (long long)s * plane, V);
+      } else if constexpr (!OCT0) {
         if (L_vsplit) vert_copy(Ts, oc.rad[s], L_vsplit + (long long)s * plane, V);
         else vert_any<OCT0, RMAX>(Ts, oc.rad[s], wp, V);
       } else {
@@ -2279,6 +2291,8 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     set_attr<true, kSW0, 8, false>();
     set_attr<true, kSW1, kUR, false>();
     set_attr<false, 0, kUR1, false>();
+    (void)hipFuncSetAttribute((const void*)k_gauss_dog<false, 0, SIFT_VS_RMAX, false, kGX, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)k_gauss_dog<false, 0, kUR96, false, 96>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     set_attr<true, kSW0, 8, true>();
@@ -2312,7 +2326,12 @@ hipError_t launch_gauss_dog(const Pyramid& P, GaussLaunch L, hipStream_t st, int
     hipLaunchKernelGGL((k_gauss_dog<true, kSW1, kUR, false>), grid, dim3(256), lds, st, P, L);
     kn = "k_gauss_dog<octave0>";
   } else {
-    hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
+    if (L.vsplit && SIFT_VS_KERNEL) {
+      hipLaunchKernelGGL((k_gauss_dog<false, 0, SIFT_VS_RMAX, false, kGX, true>), grid, dim3(256),
+                         occupancy_lds(L.o, lds), st, P, L);
+    } else {
+      hipLaunchKernelGGL((k_gauss_dog<false, 0, kUR1, false>), grid, dim3(256), occupancy_lds(L.o, lds), st, P, L);
+    }
     kn = L.vsplit ? "k_gauss_vert + k_gauss_dog<64>" : L.o == 0 ? "k_gauss_dog<octave0,fp64 base>" : "k_gauss_dog<64>";
   }
   return hipGetLastError();
