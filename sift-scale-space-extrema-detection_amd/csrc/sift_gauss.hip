@@ -846,7 +846,7 @@ __device__ __forceinline__ void rdispatch(int r, F&& f) {
 #define SIFT_BIN_TILE 1  // binary radius dispatch in the k_gauss_dog tile kernels of octaves >= 1
 #endif
 #ifndef SIFT_BIN_OCT0
-#define SIFT_BIN_OCT0 0  // ... and in octave 0's
+#define SIFT_BIN_OCT0 1  // ... and in octave 0's (bit 0: vertical pass, bit 1: horizontal: +13 VGPRs)
 #endif
 // Measured (r6f / r6g, profiles/r6g_radius_dispatch_ab.txt): 4K octave 1
 // (register window) 0.162 -> 0.149 ms, octave 2 (streamed) 0.095 -> 0.089 ms,
@@ -857,7 +857,7 @@ template <bool OCT0, int... Rs>
 __device__ __forceinline__ void vert_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
                                          const cdouble* wp, double* V) {
   constexpr int N = sizeof...(Rs) - 1;
-  if constexpr (OCT0 ? SIFT_BIN_OCT0 : SIFT_BIN_TILE) {
+  if constexpr (OCT0 ? (SIFT_BIN_OCT0 & 1) : SIFT_BIN_TILE) {
     if constexpr (OCT0) {
       rdispatch<0, N>(r, [&](auto R) { vert_o0<decltype(R)::value>(T, wp, V); });
     } else if (r <= N) {
@@ -888,7 +888,7 @@ template <bool OCT0, int... Rs>
 __device__ __forceinline__ void horz_any_(std::integer_sequence<int, Rs...>, const GTile& T, int r,
                                          const cdouble* wp, const double* V, double (&out)[kNR][4]) {
   constexpr int N = sizeof...(Rs) - 1;
-  if constexpr (OCT0 ? SIFT_BIN_OCT0 : SIFT_BIN_TILE) {
+  if constexpr (OCT0 ? (SIFT_BIN_OCT0 & 2) : SIFT_BIN_TILE) {
     if constexpr (OCT0) {
       rdispatch<0, N>(r, [&](auto R) { horz_o0<decltype(R)::value>(T, wp, V, out); });
     } else if (r <= N) {
