@@ -23,6 +23,7 @@
 // |v| within rounding of 0.8*thr go to a short list that k_exact_extrema
 // re-decides from an fp64 pointwise recompute (sift_exact.h).
 #include <cstdlib>
+#include <type_traits>
 
 #include "sift_exact.h"
 #include "sift_kernels.h"
@@ -57,6 +58,8 @@ struct XUnit {
   unsigned capa;       // ... their LDS byte address
   bool capture;        // patches are captured (L.patch or L.pre)
   long long word0;     // index of (s_first, row 0, word 0) in L.bitmap (ambiguous word list)
+  long long boff;      // lane l < NP-2: l h nw + xw (scale s_first + l, row 0, this word)
+  long long roff;      // lane l < NP-2: l h (scale s_first + l, row 0)
 };
 
 // SIFT_XGLDS: the rows stream through a per-wave LDS ring of kXRing rows
@@ -186,6 +189,21 @@ __device__ __forceinline__ unsigned x_capture(const XWin<NP>& Wn, XUnit<NP>& U, 
 #undef X_ST
 }
 
+// v_writelane_b32 (no clang builtin here): lane LANE of dst = the uniform v.
+template <int LANE>
+__device__ __forceinline__ void x_writelane(unsigned& dst, unsigned v) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(v), "i"(LANE));
+}
+
+// f(std::integral_constant<int, Q>) for Q = LO..HI in order (compile-time scale index).
+template <int LO, int HI, class F>
+__device__ __forceinline__ void x_for(F&& f) {
+  if constexpr (LO <= HI) {
+    f(std::integral_constant<int, LO>{});
+    x_for<LO + 1, HI>(f);
+  }
+}
+
 // Centre row y (slots A = y-1, B = y, C = y+1): decide every scale of the group.
 template <int NP, int A, int B, int C, bool LOWL>
 __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const ExtremaLaunch& L, int y) {
@@ -204,12 +222,17 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
     vx[q] = max3f(Wn.hx[A][q], Wn.hx[B][q], Wn.hx[C][q]);
     vn[q] = min3f(Wn.hn[A][q], Wn.hn[B][q], Wn.hn[C][q]);
   }
-  unsigned wlo = 0, whi = 0, wcnt = 0;
-  unsigned llo = 0, lhi = 0, lcnt = 0;  // LOWL: the low-contrast word
-  unsigned alo = 0, ahi = 0;            // the ambiguous word (L.ambbitmap)
+  // The row's bitmap words are built lane by lane: scale q's word (wave-
+  // uniform, in SGPRs) goes to lane q - 1 with v_writelane -- one VALU per
+  // half-word and scale; selecting it into place with a lane compare cost a
+  // v_mov + v_cndmask per half-word, count and scale (and the same again for
+  // the ambiguous word) -- a third of the scan's VALU per row.  Every lane
+  // 0..NP-3 is written each row; the other lanes' contents are never used.
+  unsigned wlo = __builtin_nondeterministic_value(0u), whi = __builtin_nondeterministic_value(0u);
+  unsigned llo = __builtin_nondeterministic_value(0u), lhi = __builtin_nondeterministic_value(0u);  // LOWL
   unsigned wsl = ~0u;                   // lane q-1: patch slot of scale q's first candidate
-#pragma unroll
-  for (int q = 1; q <= NP - 2; ++q) {
+  x_for<1, NP - 2>([&](auto qc) {
+    constexpr int q = decltype(qc)::value;
     const float v = Wn.cv[B][q];
     const float nmax = max3f(vx[q - 1], vx[q + 1], max3f(Wn.hx[A][q], Wn.hx[C][q], Wn.ex[B][q]));
     const float nmin = min3f(vn[q - 1], vn[q + 1], min3f(Wn.hn[A][q], Wn.hn[C][q], Wn.en[B][q]));
@@ -220,50 +243,43 @@ __device__ __forceinline__ void x_centre(const XWin<NP>& Wn, XUnit<NP>& U, const
         x_row_decide(v, nmax, nmin, U.colmask, L.c_lo, L.c_hi, L.exact_planes != 0, key, &L.counters[0],
                      L.ambbitmap ? nullptr : L.amb_keys, L.amb_cap, U.low, lowmask, ambmask);
 
-    if (ambmask && L.ambbitmap && U.lane == q - 1) {
-      alo = (unsigned)(ambmask >> 1);
-      ahi = (unsigned)(ambmask >> 33);
-    }
-    if (bit) {
-      const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
-      if (kXCapture && U.capture) {
-        const unsigned ps = x_capture<NP, A, B, C>(Wn, U, L, q, bit, key - U.key_base);
-        if (U.lane == q - 1) wsl = ps;
-      }
-      if (U.lane == q - 1) {
-        wlo = (unsigned)word;
-        whi = (unsigned)(word >> 32);
-        wcnt = (unsigned)__popcll(word);
-      }
-    }
-    if (LOWL && lowmask) {
-      const unsigned long long word = lowmask >> 1;
-      if (U.lane == q - 1) {
-        llo = (unsigned)word;
-        lhi = (unsigned)(word >> 32);
-        lcnt = (unsigned)__popcll(word);
-      }
-    }
-  }
-#if defined(SIFT_X_PROBE3)  // timing probe: decisions without bitmap stores
-  if (wlo == 0x12345u && whi == 0x777u) U.low += wcnt;
-  return;
-#endif
-  if (U.lane < NP - 2) {
-    const long long r = (long long)U.lane * U.h + y;
-    U.bitmap[r * U.nw + U.xw] = ((unsigned long long)whi << 32) | wlo;
-    if (kXCapture && U.capture && (wlo | whi)) L.wslot[U.word0 + r * U.nw + U.xw] = wsl;
-    if (wcnt) atomicAdd(&U.rowcount[r], wcnt);
-    if ((alo | ahi) && L.ambbitmap) {  // an ambiguous word (rare): its bits and its index for k_exact_words
-      const long long gw = U.word0 + r * U.nw + U.xw;
-      L.ambbitmap[gw] = ((unsigned long long)ahi << 32) | alo;
-      atomicAdd(&L.counters[0], (unsigned)(__popc(alo) + __popc(ahi)));
+    if (ambmask && L.ambbitmap && U.lane == 0) {  // an ambiguous word (rare): its bits and its index for k_exact_words
+      const unsigned long long aw = ambmask >> 1;  // lanes 1..62 -> bits 0..61
+      const long long gw = U.word0 + ((long long)(q - 1) * U.h + y) * U.nw + U.xw;
+      L.ambbitmap[gw] = aw;
+      atomicAdd(&L.counters[0], (unsigned)__popcll(aw));
       const unsigned slot = atomicAdd(&L.counters[kAmbWords], 1u);
       if (slot < L.amb_cap) L.amb_keys[slot] = (unsigned)gw;
     }
+    const unsigned long long word = bit >> 1;  // lanes 1..62 -> bits 0..61
+    x_writelane<q - 1>(wlo, (unsigned)word);
+    x_writelane<q - 1>(whi, (unsigned)(word >> 32));
+    if (kXCapture && U.capture && bit) {
+      const unsigned ps = x_capture<NP, A, B, C>(Wn, U, L, q, bit, key - U.key_base);
+      if (U.lane == q - 1) wsl = ps;
+    }
     if (LOWL) {
-      U.lowbitmap[r * U.nw + U.xw] = ((unsigned long long)lhi << 32) | llo;
-      if (lcnt) atomicAdd(&U.lowrowcount[r], lcnt);
+      const unsigned long long lw = lowmask >> 1;
+      x_writelane<q - 1>(llo, (unsigned)lw);
+      x_writelane<q - 1>(lhi, (unsigned)(lw >> 32));
+    }
+  });
+#if defined(SIFT_X_PROBE3)  // timing probe: decisions without bitmap stores
+  if (wlo == 0x12345u && whi == 0x777u) U.low += 1;
+  return;
+#endif
+  if (U.lane < NP - 2) {
+    // lane l stores scale s_first + l's word of row y: a uniform row pointer
+    // plus the lane's (scale, word) offset
+    const unsigned long long* const brow = U.bitmap + (long long)y * U.nw;
+    const_cast<unsigned long long*>(brow)[U.boff] = ((unsigned long long)whi << 32) | wlo;
+    if (kXCapture && U.capture && (wlo | whi)) L.wslot[U.word0 + ((long long)U.lane * U.h + y) * U.nw + U.xw] = wsl;
+    const unsigned wcnt = (unsigned)(__popc(wlo) + __popc(whi));
+    if (wcnt) atomicAdd(&U.rowcount[U.roff + y], wcnt);
+    if (LOWL) {
+      const_cast<unsigned long long*>(U.lowbitmap + (long long)y * U.nw)[U.boff] = ((unsigned long long)lhi << 32) | llo;
+      const unsigned lcnt = (unsigned)(__popc(llo) + __popc(lhi));
+      if (lcnt) atomicAdd(&U.lowrowcount[U.roff + y], lcnt);
     }
   }
 }
@@ -356,6 +372,8 @@ __device__ __forceinline__ void x_scan(const Pyramid& P, const ExtremaLaunch& L,
   const long long rb = (long long)b * L.rows_per_img + L.row_off[o] + (s_first - 1) * oc.h;
   U.bitmap = L.bitmap + wb;
   U.word0 = wb;
+  U.boff = ((long long)U.lane * U.h) * U.nw + xw;
+  U.roff = (long long)U.lane * U.h;
   U.rowcount = L.rowcount + rb;
   if (LOWL) {
     U.lowbitmap = L.lowbitmap + wb;

@@ -98,7 +98,10 @@ __device__ __forceinline__ unsigned long long x_row_decide(float v, float nmax, 
                                                            unsigned long long& lowmask, unsigned long long& ambmask) {
   lowmask = 0ull;
   ambmask = 0ull;
-  const unsigned long long ext_any = __ballot(v >= nmax || v <= nmin) & colmask;
+  // two compare masks OR-ed in SALU (a ballot of the || goes through a
+  // v_cndmask + v_cmp of the combined lane bool: 2 VALU per scale and row)
+  const unsigned long long ext_any =
+      (__builtin_amdgcn_ballot_w64(v >= nmax) | __builtin_amdgcn_ballot_w64(v <= nmin)) & colmask;
   if (!ext_any) return 0ull;
   const float av = __builtin_fabsf(v);
   const unsigned long long gt = __ballot(v > nmax), lt = __ballot(v < nmin);
