@@ -40,6 +40,7 @@ offsets, all_gather_into_tensor, merge by argsort on the device).  K is
 chosen by a cost model of the critical path (octave_cost).
 """
 import math
+import os
 import time
 
 import numpy as np
@@ -117,6 +118,10 @@ def plan_bands(width, height, params, n_shards, max_overhead=0.5):
         t = frac * sum(cost[:K + 1]) + sum(cost[K + 1:])
         if best is None or t < best[0]:
             best = (t, K, crops)
+    forced = os.environ.get("SIFT_SHARD_K")  # experiments: force the split octave (clamped to the margin's bound)
+    if forced is not None:
+        K = max(0, min(k_max, int(forced)))
+        return BandPlan(width, height, O, K, bands, crops_for(K))
     return BandPlan(width, height, O, best[1], bands, best[2])
 
 
