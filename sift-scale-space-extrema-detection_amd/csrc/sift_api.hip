@@ -197,6 +197,17 @@ struct sift_ctx {
   DBuf seedv;                                  // vertical sums of the seed-only octaves (launch_seed_only)
   long long vsplit_pi = 0;                     // ... doubles per image of a batch
   std::vector<double> wts_host;                // taps last uploaded to wts
+  // Taps of the deepest schedule built so far (setup_geometry): per-(octave,
+  // scale) sigma, the padded tap vector, its length after each octave, and
+  // every scale's radius and tap offset.  Sigma does not depend on the octave
+  // count, so a schedule whose sigmas are a prefix of these reuses a prefix
+  // of the taps instead of ~3 K exp() per call (8K O6 S5: ~35 us).
+  struct TapCache {
+    int NS = 0;
+    std::vector<double> sigma, w;
+    std::vector<size_t> oct_end;
+    std::vector<int> rad, wofs;
+  } taps;
   DBuf bitmap, rowcount, rowoff, amb_keys;     // extrema scan
   DBuf ambbitmap;                              // ambiguous words (k_exact_words)
   bool x_words = false;                        // this extrema stage lists ambiguous words, not keys
@@ -483,6 +494,11 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
   std::vector<double> w;
   long long goff = 0, doff = 0, soff = 0;
   unsigned long long koff = 0;
+  sift_ctx::TapCache& tc = ctx->taps;
+  const bool taps_hit = need_weights && tc.NS == NS && tc.sigma.size() >= (size_t)O * NS &&
+                        std::equal(ctx->sigma.begin(), ctx->sigma.end(), tc.sigma.begin());
+  if (taps_hit) w.assign(tc.w.begin(), tc.w.begin() + (std::ptrdiff_t)tc.oct_end[O - 1]);
+  std::vector<size_t> oct_end;
   for (int o = 0; o < O; ++o) {
     Octave& oc = P.oct[o];
     oc.h = ctx->dims[2 * o];
@@ -499,6 +515,14 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
     doff += ND * plane;
     oc.rmax = 0;
     oc.l64_off = -1;
+    if (taps_hit) {
+      for (int s = 0; s < NS; ++s) {
+        oc.rad[s] = tc.rad[o * NS + s];
+        oc.wofs[s] = tc.wofs[o * NS + s];
+        oc.rmax = std::max(oc.rmax, oc.rad[s]);
+      }
+      continue;
+    }
     for (int s = 0; s < NS; ++s) {
       const double sg = ctx->sigma[o * NS + s];
       int r = 0;
@@ -524,8 +548,24 @@ static int setup_geometry(sift_ctx* ctx, int W, int H, const sift_params* p, con
       oc.rad[s] = r;
       oc.rmax = std::max(oc.rmax, r);
     }
+    oct_end.push_back(w.size());
   }
   if (koff > 0xffffffffull) return set_err(ctx, SIFT_E_UNSUPPORTED, "image too large for 32-bit keys");
+  if (need_weights && !taps_hit && (tc.NS != NS || O * NS >= (int)tc.sigma.size())) {
+    // a miss at this depth or deeper replaces the cache; a shallower miss
+    // (another schedule) leaves a deeper one in place
+    tc.NS = NS;
+    tc.sigma = ctx->sigma;
+    tc.w = w;
+    tc.oct_end = oct_end;
+    tc.rad.assign((size_t)O * NS, 0);
+    tc.wofs.assign((size_t)O * NS, 0);
+    for (int o = 0; o < O; ++o)
+      for (int s = 0; s < NS; ++s) {
+        tc.rad[o * NS + s] = P.oct[o].rad[s];
+        tc.wofs[o * NS + s] = P.oct[o].wofs[s];
+      }
+  }
   P.nimg = 1;  // one image (build_common sets a batch)
   P.kpi = (unsigned)koff;
   // LDS feasibility of the Gaussian kernel (two strips of 32 rows x (76 + 2R) fp64).
