@@ -342,6 +342,27 @@ def test_detect_is_deterministic(gpu_ctx):
     assert a.tobytes() == b.tobytes()
 
 
+def test_schedule_taps_reused_across_depths_and_schedules(gpu_ctx):
+    """The context keeps the deepest schedule's taps (setup_geometry) and a
+    schedule whose sigmas are its prefix reuses them: detections alternating
+    octave counts, scale counts and blurs on one context equal the same
+    detections on fresh contexts, byte for byte."""
+    img = blob_image(200, 150, seed=41)
+    seq = [(5, 4, 0.8), (3, 4, 0.8), (5, 4, 0.8), (4, 3, 0.8), (2, 4, 0.8), (5, 4, 1.1), (3, 4, 1.1), (4, 4, 0.8)]
+    ctx = sift_amd.Context(0)
+    try:
+        for O, S, mb in seq:
+            p = sift_amd.make_params(O, S, min_blur=mb)
+            fresh = sift_amd.Context(0)
+            try:
+                want = fresh.detect(img, p).tobytes()
+            finally:
+                fresh.close()
+            assert ctx.detect(img, p).tobytes() == want, (O, S, mb)
+    finally:
+        ctx.close()
+
+
 def test_skip_gauss_planes_same_keypoints(gpu_ctx):
     img = blob_image(300, 200, seed=24)
     a = gpu_ctx.detect(img, sift_amd.make_params(4, 4))
